@@ -1,0 +1,140 @@
+/*
+ * dcol.h — C-ABI of the MI355X-native batched differentiable-proximity engine.
+ *
+ * Drop-in boundary for the reference's proximity hot path
+ * (CogSP/DCOL-trajectory-optimization):
+ *
+ *   reference                                                 replaced by
+ *   ------------------------------------------------------   ---------------------------------
+ *   primitive objects consumed by problem_matrices()          dcol_table_create()
+ *     primitives/misc_primitive_constructor.py:4-88             (static shape table, uploaded
+ *     primitives/problem_matrices.py:255-364                     once to HBM)
+ *   proximity_mrp(prim1, prim2, pdip_tol) -> (alpha, x[:3])   dcol_plan_run(flags=CONTACT)
+ *     proximity/proximity.py:6-54                             dcol_prox_batch_host()
+ *   proximity_gradient(prim1, prim2, pdip_tol)                dcol_plan_run(flags=GRAD_FD)
+ *     -> (alpha, d_alpha/d[r1,p1,r2,p2])                      dcol_prox_batch_host()
+ *     proximity/proximity_gradient.py:91-138
+ *   combine_problem_matrices() + solve_lp_pdip()              inside the device kernel
+ *     primitives/combine_problem_matrices.py:3-70,
+ *     proximity/pdip.py:291-470, proximity/NT/NT_scaling.py
+ *
+ * One call handles a whole batch of (knot x primitive-pair) problems.  All arithmetic is
+ * IEEE FP64.  Plain pointers and sizes only; no torch types.  Error behaviour: every entry
+ * point returns an int (DCOL_SUCCESS or a negative DCOL_ERR_*); per-pair solver outcomes
+ * are reported in a status[] array (enum dcol_status), which the Python shim maps back to
+ * the reference's exception types (bare Exception at 50 iterations, pdip.py:470;
+ * ValueError for unsupported pairs, combine_problem_matrices.py:70; LinAlgError for a
+ * non-PD normal matrix, pdip.py:317/:434).
+ */
+#ifndef DCOL_H
+#define DCOL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCOL_ABI_VERSION 1
+
+/* Primitive types (misc_primitive_constructor.py:4-88). */
+enum dcol_shape_type {
+    DCOL_POLYTOPE = 0, /* A (nh x 3), b (nh)          PolytopeMRP  */
+    DCOL_SPHERE = 1,   /* R                           SphereMRP    */
+    DCOL_CONE = 2,     /* H, beta (half angle, rad)   ConeMRP      */
+    DCOL_CAPSULE = 3,  /* R, L                        CapsuleMRP   */
+    DCOL_CYLINDER = 4, /* R, L                        CylinderMRP  */
+    DCOL_POLYGON = 5   /* A (nh x 2), b (nh), R       PolygonMRP   */
+};
+
+/* Per-pair outcome. */
+enum dcol_status {
+    DCOL_OK = 0,
+    DCOL_MAXITER = 1,     /* no convergence within max_iter (reference: 50, pdip.py:408)  */
+    DCOL_UNSUPPORTED = 2, /* both primitives have extra columns (combine case 4)          */
+    DCOL_NOT_PD = 3,      /* Cholesky of G'G or of the NT normal matrix failed            */
+    DCOL_NONFINITE = 4,   /* a non-finite value reached a factorisation                   */
+    DCOL_TOO_LARGE = 5    /* more orthant rows than the engine's row capacity (32)        */
+};
+
+/* dcol_plan_run / dcol_prox_batch_host flags. */
+enum dcol_flags {
+    DCOL_GRAD_FD = 1,       /* d alpha / d[r1,p1,r2,p2] by 2-point forward differences of
+                               z'(G(theta)x - h(theta)), step sqrt(eps) (reference mode,
+                               proximity_gradient.py:50-88)                               */
+    DCOL_GRAD_ENVELOPE = 2, /* the same gradient in closed form (envelope theorem)       */
+    DCOL_CONTACT = 4        /* write x[0:3] (proximity.py:51-54)                          */
+};
+
+/* Return codes of every entry point. */
+#define DCOL_SUCCESS 0
+#define DCOL_ERR_ARG (-1)
+#define DCOL_ERR_HIP (-2)
+#define DCOL_ERR_NOMEM (-3)
+
+/* One primitive (all fields read; unused ones ignored for the type). */
+typedef struct dcol_shape_desc {
+    int32_t type;        /* enum dcol_shape_type                                      */
+    int32_t nh;          /* faces: rows of A (polytope / polygon), else 0             */
+    const double* A;     /* row-major nh x 3 (polytope) or nh x 2 (polygon), or NULL  */
+    const double* b;     /* nh, or NULL                                               */
+    double R, L, H, beta;
+    double r_offset[3];  /* body-frame position offset (problem_matrices.py:281)      */
+    double Q_offset[9];  /* row-major 3x3 orientation offset (problem_matrices.py:282) */
+} dcol_shape_desc;
+
+typedef struct dcol_table dcol_table; /* device-resident shape table */
+typedef struct dcol_plan dcol_plan;   /* static pairing -> kernel-variant buckets */
+
+/* ---- library / errors --------------------------------------------------------------- */
+int dcol_abi_version(void);
+const char* dcol_status_string(int32_t status);
+const char* dcol_last_error(void); /* thread-local message of the last failing call */
+int dcol_device_count(int32_t* count);
+
+/* ---- shape table ---------------------------------------------------------------------
+ * Copies the descriptors (and A/b) into an immutable table in HBM of `device`.       */
+int dcol_table_create(const dcol_shape_desc* shapes, int32_t n, int32_t device, dcol_table** out);
+int dcol_table_destroy(dcol_table* table);
+int dcol_table_size(const dcol_table* table, int32_t* n);
+/* Problem size of a pair (m rows, n columns, number of SOC blocks); returns the pair's
+ * static status (DCOL_OK, DCOL_UNSUPPORTED or DCOL_TOO_LARGE) in *status.            */
+int dcol_pair_dims(const dcol_table* table, int32_t s1, int32_t s2, int32_t* m, int32_t* n,
+                   int32_t* n_soc, int32_t* status);
+
+/* ---- plans ---------------------------------------------------------------------------
+ * A plan fixes the pairing (shape ids, HOST arrays of length B) and buckets the pairs by
+ * kernel variant.  It is reusable for any poses: ALTRO evaluates the same
+ * (knot x obstacle) pairing at every iteration (systems/*.py inequality_constraints_x). */
+int dcol_plan_create(const dcol_table* table, int64_t B, const int32_t* shape1,
+                     const int32_t* shape2, dcol_plan** out);
+int dcol_plan_destroy(dcol_plan* plan);
+int dcol_plan_num_launches(const dcol_plan* plan, int32_t* n);
+
+/* Solve every pair of the plan.  All arrays are DEVICE pointers on the table's device,
+ * structure-of-arrays:
+ *   pose1, pose2 : [6][B]  (rows r_x r_y r_z p_x p_y p_z; p = MRP)
+ *   alpha        : [B]      minimum uniform scaling (x[3])
+ *   contact      : [3][B]   x[0:3]            (written if flags & DCOL_CONTACT, else may be NULL)
+ *   grad         : [12][B]  d alpha/d[r1,p1,r2,p2] (if a GRAD flag is set, else may be NULL)
+ *   iters        : [B]      Newton steps taken (may be NULL)
+ *   status       : [B]      enum dcol_status (may be NULL)
+ * tol is pdip_tol (reference default 1e-6); max_iter the iteration cap (reference: 50).
+ * Asynchronous on `stream` (a hipStream_t, NULL = default stream); no allocation and no
+ * synchronisation, so the call can be captured into a hipGraph.                        */
+int dcol_plan_run(const dcol_plan* plan, const double* pose1, const double* pose2, double tol,
+                  int32_t max_iter, int32_t flags, double* alpha, double* contact, double* grad,
+                  int32_t* iters, int32_t* status, void* stream);
+
+/* Convenience: HOST arrays in, HOST arrays out, synchronous.  Array-of-structures rows:
+ * pose1/pose2 B x 6, contact B x 3, grad B x 12.  Builds a transient plan; staging
+ * buffers are owned by the table (calls on one table are serialised).               */
+int dcol_prox_batch_host(const dcol_table* table, int64_t B, const int32_t* shape1,
+                         const int32_t* shape2, const double* pose1, const double* pose2,
+                         double tol, int32_t max_iter, int32_t flags, double* alpha,
+                         double* contact, double* grad, int32_t* iters, int32_t* status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DCOL_H */
