@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""Benchmark: PDIP proximity + gradient pair-solves/sec on MI355X.
+
+Workload (BASELINE.json configs[3], "synthetic 100k random polytope-polytope pairs"):
+per GPU, B = 100,000 (knot x primitive-pair) problems; primitives are rect-prism polytopes
+(nh = 6) drawn from a 64-entry shape table with dims ~ U(0.2, 2)^3 (shape ids uniform per
+pair); poses r ~ U(-3, 3)^3, p (MRP) ~ U(-1, 1)^3; seed 0 (+ rank).  One "step" = one
+dcol_plan_run over the whole batch: conic assembly + PDIP (pdip_tol 1e-6) + the 12-gradient
+(FD mode = the reference's formulation) + alpha, with poses already resident in HBM.
+
+Multi-GPU: one process per GPU (torchrun); every rank solves its own 100k-pair shard
+(independent units, no data-path collective) -> "scaling": "weak"; the timed region is
+bracketed by barrier + synchronize and the max over ranks is taken.
+
+Also reported: roofline of the solve kernel (HIP-event timed on the launch stream) against
+HBM (algorithmic 208 B/pair) and against FP64 vector peak; the CPU baseline = the NumPy
+restatement of the reference (oracle/, test infrastructure) on a bounded sample on the
+host cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "dcol-trajectory-optimization_amd")
+for _p in (PKG, REPO):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
+FP64_VECTOR_PEAK_TFS = 78.6    # MI355X FP64 vector peak (AMD spec)
+BYTES_PER_PAIR = 208           # poses 2x6 f64 + 2 int32 ids in; alpha + 12 grad f64 out
+
+
+def shape_table(n_shapes=64, seed=0):
+    """Array-form shape table of random rect prisms (tests/golden layout)."""
+    rng = np.random.default_rng(seed)
+    A = np.array([[1.0, 0, 0], [0, 1, 0], [0, 0, 1], [-1, 0, 0], [0, -1, 0], [0, 0, -1]])
+    dims = rng.uniform(0.2, 2.0, (n_shapes, 3))
+    b = np.concatenate([dims / 2, dims / 2], axis=1)
+    return {"type": np.zeros(n_shapes, np.int32), "nh": np.full(n_shapes, 6, np.int32),
+            "A_off": np.arange(n_shapes, dtype=np.int32) * 6, "A_pool": np.tile(A, (n_shapes, 1)),
+            "b_pool": b.reshape(-1), "params": np.zeros((n_shapes, 4)),
+            "r_offset": np.zeros((n_shapes, 3)), "Q_offset": np.tile(np.eye(3), (n_shapes, 1, 1))}
+
+
+def pairs(B, n_shapes, seed):
+    rng = np.random.default_rng(seed)
+    s1 = rng.integers(0, n_shapes, B).astype(np.int32)
+    s2 = rng.integers(0, n_shapes, B).astype(np.int32)
+    pose1 = np.hstack([rng.uniform(-3, 3, (B, 3)), rng.uniform(-1, 1, (B, 3))])
+    pose2 = np.hstack([rng.uniform(-3, 3, (B, 3)), rng.uniform(-1, 1, (B, 3))])
+    return s1, s2, pose1, pose2
+
+
+def _oracle_chunk(args):
+    tab, s1, s2, p1, p2 = args
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    from oracle import dcol_oracle as O
+    t0 = time.perf_counter()
+    out = O.run_batch(tab, s1, s2, p1, p2, 1e-6, True)
+    return time.perf_counter() - t0, out["status"]
+
+
+def cpu_baseline(tab, s1, s2, p1, p2, sample, workers):
+    """NumPy restatement of the reference (oracle/, a 'port'), one process per core."""
+    import multiprocessing as mp
+    n = min(sample, len(s1))
+    chunks = np.array_split(np.arange(n), workers)
+    jobs = [(tab, s1[c], s2[c], p1[c], p2[c]) for c in chunks if len(c)]
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(len(jobs)) as pool:
+        res = pool.map(_oracle_chunk, jobs)
+    wall = time.perf_counter() - t0
+    cpu_s = sum(r[0] for r in res)
+    return {"value": n / wall, "unit": "pair-solves/s", "cores": len(jobs), "kind": "port",
+            "sample": f"{n} of the same synthetic poly-poly pairs, proximity+FD gradient, NumPy oracle "
+                      f"(oracle/dcol_oracle.py), {len(jobs)} processes, {cpu_s:.1f} s CPU, {wall:.1f} s wall",
+            "per_core": n / cpu_s}
+
+
+def read_traffic(profile_dir, kernel_substr="prox_kernel"):
+    """Per-launch HBM bytes of the solve kernel from a committed rocprofv3 PMC pass
+    (FETCH_SIZE + WRITE_SIZE in KB; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM)."""
+    path = os.path.join(profile_dir, "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        return d.get("bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--pairs", type=int, default=100_000, help="pairs per GPU")
+    ap.add_argument("--grad", choices=["fd", "envelope"], default="fd")
+    ap.add_argument("--cpu-sample", type=int, default=4000)
+    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--check", type=int, default=256, help="pairs re-checked against the oracle")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local)
+
+    from dcol_amd import Engine, spec_from_arrays
+    tab = shape_table()
+    B = args.pairs
+    s1, s2, p1, p2 = pairs(B, len(tab["type"]), seed=1000 + rank)
+    eng = Engine(device=local)
+    ids = np.array([eng.register(spec_from_arrays(tab, k)) for k in range(len(tab["type"]))], np.int32)
+    plan = eng.plan(ids[s1], ids[s2])
+    pose1 = torch.from_numpy(np.ascontiguousarray(p1.T)).to(dev)
+    pose2 = torch.from_numpy(np.ascontiguousarray(p2.T)).to(dev)
+    from dcol_amd import alloc_outputs
+    out = alloc_outputs(B, dev, want_grad=True, want_contact=False)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        plan.run(pose1, pose2, grad=args.grad, contact=False, out=out, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    # kernel-only timing: HIP events on the launch stream
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        step()
+        ev[k][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if dist is not None:
+        t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms_max = float(t[0]), float(t[1])
+    else:
+        kern_ms_max = kern_ms
+
+    status = out["status"].cpu().numpy()
+    iters = out["iters"].cpu().numpy()
+    alpha = out["alpha"].cpu().numpy()
+    grad = out["grad"].cpu().numpy()
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    total = B * world * args.steps
+    value = total / elapsed
+    achieved_gbs = BYTES_PER_PAIR * B / (kern_ms * 1e-3) / 1e9
+    traffic = read_traffic(os.path.join(REPO, "profiles"))
+    flops_pair = flops_per_pair(iters[status == 0])
+    line = {
+        "metric": "PDIP proximity+grad pair-solves/sec",
+        "value": value,
+        "unit": "pair-solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": "synthetic random polytope-polytope pairs (BASELINE.json configs[3])",
+                   "pairs_per_gpu": B, "shape_table": "64 rect prisms, dims U(0.2,2)^3",
+                   "poses": "r U(-3,3)^3, p U(-1,1)^3", "pdip_tol": 1e-6, "gradient": args.grad,
+                   "parallelism": f"dp{world} (independent pair shards)"},
+        "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic},
+        "roofline_fp64": {"bound": "fp64-valu", "achieved": flops_pair * B / (kern_ms * 1e-3) / 1e12,
+                          "peak": FP64_VECTOR_PEAK_TFS, "unit": "TFLOP/s",
+                          "frac": flops_pair * B / (kern_ms * 1e-3) / 1e12 / FP64_VECTOR_PEAK_TFS,
+                          "flops_per_pair": flops_pair},
+        "kernel_ms": kern_ms,
+        "kernel_ms_max_rank": kern_ms_max,
+        "solve_stats": {"ok_frac": float(np.mean(status == 0)), "iters_mean": float(iters[status == 0].mean()),
+                        "iters_max": int(iters.max())},
+    }
+    # spot parity check against the oracle on the first pairs of the timed batch
+    if args.check:
+        from oracle import dcol_oracle as O
+        n = min(args.check, B)
+        ref = O.run_batch(tab, s1[:n], s2[:n], p1[:n], p2[:n], 1e-6, True)
+        ok = ref["status"] == 0
+        a_ok = np.all(np.abs(alpha[:n][ok] - ref["alpha"][ok]) <= 1e-6 * np.abs(ref["alpha"][ok]) + 1e-12)
+        g_ok = np.all(np.abs(grad[:, :n].T[ok] - ref["grad"][ok]).max(1)
+                      <= 1e-5 * np.maximum(np.abs(ref["grad"][ok]).max(1), 1))
+        line["parity_check"] = {"pairs": int(n), "status_equal": bool(np.array_equal(status[:n], ref["status"])),
+                                "alpha_ok": bool(a_ok), "grad_ok": bool(g_ok)}
+    if world == 1 and not args.no_cpu:
+        workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
+        line["cpu_baseline"] = cpu_baseline(tab, s1, s2, p1, p2, args.cpu_sample, workers)
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def flops_per_pair(iters):
+    """Algorithmic FP64 operation count per pair, poly6 x poly6 (m = 12, n = 4), from the
+    hand model of SURVEY.md §8d (each +,-,*,/,sqrt = 1, following pdip.py/NT_scaling.py):
+    assembly 530 + init 777 + iters x 1682 + exit iteration 276 + FD gradient 8485."""
+    it = float(np.mean(iters)) if len(iters) else 7.0
+    return 530 + 777 + it * 1682 + 276 + 8485
+
+
+if __name__ == "__main__":
+    main()

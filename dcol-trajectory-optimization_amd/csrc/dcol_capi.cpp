@@ -1,0 +1,407 @@
+// dcol_capi.cpp — host side of the C-ABI declared in include/dcol.h.
+//
+//  * dcol_table_create: digests the primitive descriptors into DevShape records and a pool
+//    of orthant-row descriptors (DevRow), uploaded once to HBM.  This is the static part of
+//    problem_matrices() (primitives/problem_matrices.py:4-209): the per-type constant rows;
+//    the pose-dependent part (DCM, rotation, h) runs inside the kernel.
+//  * dcol_plan_create: classifies each pair (combine_problem_matrices.py:3-70 cases 1-3 vs
+//    the unsupported case 4) and buckets pairs by kernel variant (N, NSOC, OMAX).
+//  * dcol_plan_run: one kernel launch per non-empty bucket, asynchronous on the caller's
+//    stream, no allocation (graph-capturable).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/dcol.h"
+#include "dcol_device.hpp"
+#include "dcol_host.hpp"
+#include "dcol_launch.hpp"
+
+using namespace dcol;
+using namespace dcol_host;
+
+namespace {
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(DCOL_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+namespace dcol {
+// pairs rejected on the host (unsupported combination / too many rows)
+__global__ void __launch_bounds__(256) reject_kernel(KArgs A, int32_t code) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= A.n) return;
+    const int64_t pi = A.perm ? (int64_t)A.perm[A.slot0 + t] : (A.slot0 + t);
+    const int64_t B = A.B;
+    const double nan = __builtin_nan("");
+    A.alpha[pi] = nan;
+    if (A.iters) A.iters[pi] = 0;
+    if (A.status) A.status[pi] = code;
+    if ((A.flags & F_CONTACT) && A.contact)
+        for (int q = 0; q < 3; ++q) A.contact[q * B + pi] = nan;
+    if ((A.flags & (F_GRAD_FD | F_GRAD_ENV)) && A.grad)
+        for (int q = 0; q < 12; ++q) A.grad[q * B + pi] = nan;
+}
+
+}  // namespace dcol
+
+struct dcol_table {
+    int device = 0;
+    std::vector<DevShape> shapes;
+    std::vector<DevRow> rows;
+    DevShape* d_shapes = nullptr;
+    DevRow* d_rows = nullptr;
+    // staging for dcol_prox_batch_host
+    std::mutex mu;
+    void* stage = nullptr;
+    size_t stage_bytes = 0;
+};
+
+struct Launch {
+    int kind;       // 0 = solve, 1 = reject
+    int N, nsoc, omax;
+    int32_t code;   // reject status
+    int64_t slot0, n;
+};
+
+struct dcol_plan {
+    const dcol_table* table = nullptr;
+    int64_t B = 0;
+    int32_t* d_s1 = nullptr;
+    int32_t* d_s2 = nullptr;
+    int32_t* d_perm = nullptr;   // nullptr when the whole batch is one variant
+    bool owns = false;           // device arrays owned (false: views into table staging)
+    std::vector<Launch> launches;
+};
+
+namespace {
+
+hipError_t launch_variant(int N, int nsoc, int omax, const KArgs& a, hipStream_t st) {
+    const int64_t grid = (a.n + kBlock - 1) / kBlock;
+    if (N == 4) return launch_n4(nsoc, omax, a, grid, st);
+    if (N == 5) return launch_n5(nsoc, omax, a, grid, st);
+    if (N == 6) return launch_n6(nsoc, omax, a, grid, st);
+    return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dcol_abi_version(void) { return DCOL_ABI_VERSION; }
+
+const char* dcol_status_string(int32_t s) {
+    switch (s) {
+        case DCOL_OK: return "ok";
+        case DCOL_MAXITER: return "Maximum number of iterations reached, PDIP failed";
+        case DCOL_UNSUPPORTED: return "Failed to combine problem matrices.";
+        case DCOL_NOT_PD: return "Matrix is not positive definite";
+        case DCOL_NONFINITE: return "array must not contain infs or NaNs";
+        case DCOL_TOO_LARGE: return "pair exceeds the engine's orthant-row capacity";
+        default: return "unknown status";
+    }
+}
+
+const char* dcol_last_error(void) { return last_error().c_str(); }
+
+int dcol_device_count(int32_t* count) {
+    if (!count) return fail(DCOL_ERR_ARG, "count is NULL");
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    *count = n;
+    return DCOL_SUCCESS;
+}
+
+int dcol_table_create(const dcol_shape_desc* shapes, int32_t n, int32_t device, dcol_table** out) {
+    if (!out || n < 0 || (n > 0 && !shapes)) return fail(DCOL_ERR_ARG, "dcol_table_create: bad arguments");
+    *out = nullptr;
+    auto* t = new (std::nothrow) dcol_table();
+    if (!t) return fail(DCOL_ERR_NOMEM, "host allocation failed");
+    t->device = device;
+    t->shapes.resize(n);
+    for (int32_t i = 0; i < n; ++i) {
+        int rc = digest_shape(shapes[i], i, t->shapes[i], t->rows);
+        if (rc != DCOL_SUCCESS) {
+            delete t;
+            return rc;
+        }
+    }
+    if (t->rows.empty()) t->rows.resize(1);   // keep a valid device pointer
+    if (t->shapes.empty()) t->shapes.resize(1);
+    DeviceGuard g(device);
+    hipError_t e = hipMalloc(&t->d_shapes, sizeof(DevShape) * t->shapes.size());
+    if (e == hipSuccess) e = hipMalloc(&t->d_rows, sizeof(DevRow) * t->rows.size());
+    if (e == hipSuccess) e = hipMemcpy(t->d_shapes, t->shapes.data(), sizeof(DevShape) * t->shapes.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(t->d_rows, t->rows.data(), sizeof(DevRow) * t->rows.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (t->d_shapes) (void)hipFree(t->d_shapes);
+        if (t->d_rows) (void)hipFree(t->d_rows);
+        delete t;
+        return fail(DCOL_ERR_HIP, std::string("dcol_table_create: ") + hipGetErrorString(e));
+    }
+    t->shapes.resize(n);
+    *out = t;
+    return DCOL_SUCCESS;
+}
+
+int dcol_table_destroy(dcol_table* t) {
+    if (!t) return DCOL_SUCCESS;
+    DeviceGuard g(t->device);
+    if (t->d_shapes) (void)hipFree(t->d_shapes);
+    if (t->d_rows) (void)hipFree(t->d_rows);
+    if (t->stage) (void)hipFree(t->stage);
+    delete t;
+    return DCOL_SUCCESS;
+}
+
+int dcol_table_size(const dcol_table* t, int32_t* n) {
+    if (!t || !n) return fail(DCOL_ERR_ARG, "dcol_table_size: NULL argument");
+    *n = (int32_t)t->shapes.size();
+    return DCOL_SUCCESS;
+}
+
+int dcol_pair_dims(const dcol_table* t, int32_t s1, int32_t s2, int32_t* m, int32_t* n, int32_t* n_soc, int32_t* status) {
+    if (!t) return fail(DCOL_ERR_ARG, "dcol_pair_dims: NULL table");
+    const int32_t ns = (int32_t)t->shapes.size();
+    if (s1 < 0 || s1 >= ns || s2 < 0 || s2 >= ns) return fail(DCOL_ERR_ARG, "dcol_pair_dims: shape id out of range");
+    const DevShape& a = t->shapes[s1];
+    const DevShape& b = t->shapes[s2];
+    PairClass c = classify(a, b);
+    const int q1 = a.soc_kind == SOC_NONE ? 0 : (a.soc_kind == SOC_CONE ? 3 : 4);
+    const int q2 = b.soc_kind == SOC_NONE ? 0 : (b.soc_kind == SOC_CONE ? 3 : 4);
+    if (m) *m = c.o + q1 + q2;
+    if (n) *n = c.N;
+    if (n_soc) *n_soc = c.nsoc;
+    if (status) *status = c.status;
+    return DCOL_SUCCESS;
+}
+
+}  // extern "C"
+
+namespace {
+// Classify + bucket (counting sort by variant key).  Fills p->launches and the slot->pair
+// permutation; returns DCOL_SUCCESS or an error.
+int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, dcol_plan* p,
+                 std::vector<int32_t>& perm) {
+    const int32_t ns = (int32_t)t->shapes.size();
+    using Key = std::tuple<int, int, int, int, int>;   // kind, N, nsoc, omax, code
+    std::map<Key, std::vector<int32_t>> groups;
+    for (int64_t i = 0; i < B; ++i) {
+        if (s1[i] < 0 || s1[i] >= ns || s2[i] < 0 || s2[i] >= ns)
+            return fail(DCOL_ERR_ARG, "shape id out of range at pair " + std::to_string(i));
+        PairClass c = classify(t->shapes[s1[i]], t->shapes[s2[i]]);
+        Key k = c.status == DCOL_OK ? Key{0, c.N, c.nsoc, c.omax, 0} : Key{1, 0, 0, 0, c.status};
+        groups[k].push_back((int32_t)i);
+    }
+    p->table = t;
+    p->B = B;
+    p->launches.clear();
+    perm.clear();
+    perm.reserve(B);
+    for (auto& kv : groups) {
+        Launch L;
+        L.kind = std::get<0>(kv.first);
+        L.N = std::get<1>(kv.first);
+        L.nsoc = std::get<2>(kv.first);
+        L.omax = std::get<3>(kv.first);
+        L.code = std::get<4>(kv.first);
+        L.slot0 = (int64_t)perm.size();
+        L.n = (int64_t)kv.second.size();
+        perm.insert(perm.end(), kv.second.begin(), kv.second.end());
+        p->launches.push_back(L);
+    }
+    return DCOL_SUCCESS;
+}
+}  // namespace
+
+extern "C" {
+
+int dcol_plan_create(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, dcol_plan** out) {
+    if (!t || !out || B < 0 || (B > 0 && (!s1 || !s2))) return fail(DCOL_ERR_ARG, "dcol_plan_create: bad arguments");
+    if (B > INT32_MAX) return fail(DCOL_ERR_ARG, "dcol_plan_create: B exceeds 2^31-1");
+    *out = nullptr;
+    auto* p = new (std::nothrow) dcol_plan();
+    if (!p) return fail(DCOL_ERR_NOMEM, "host allocation failed");
+    std::vector<int32_t> perm;
+    int rc = bucket_pairs(t, B, s1, s2, p, perm);
+    if (rc != DCOL_SUCCESS) {
+        delete p;
+        return rc;
+    }
+    p->owns = true;
+    if (B == 0) {
+        *out = p;
+        return DCOL_SUCCESS;
+    }
+    DeviceGuard g(t->device);
+    hipError_t e = hipMalloc(&p->d_s1, sizeof(int32_t) * B);
+    if (e == hipSuccess) e = hipMalloc(&p->d_s2, sizeof(int32_t) * B);
+    if (e == hipSuccess) e = hipMemcpy(p->d_s1, s1, sizeof(int32_t) * B, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->d_s2, s2, sizeof(int32_t) * B, hipMemcpyHostToDevice);
+    if (e == hipSuccess && p->launches.size() > 1) {
+        e = hipMalloc(&p->d_perm, sizeof(int32_t) * B);
+        if (e == hipSuccess) e = hipMemcpy(p->d_perm, perm.data(), sizeof(int32_t) * B, hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) {
+        dcol_plan_destroy(p);
+        return fail(DCOL_ERR_HIP, std::string("dcol_plan_create: ") + hipGetErrorString(e));
+    }
+    *out = p;
+    return DCOL_SUCCESS;
+}
+
+int dcol_plan_destroy(dcol_plan* p) {
+    if (!p) return DCOL_SUCCESS;
+    if (p->table && p->owns) {
+        DeviceGuard g(p->table->device);
+        if (p->d_s1) (void)hipFree(p->d_s1);
+        if (p->d_s2) (void)hipFree(p->d_s2);
+        if (p->d_perm) (void)hipFree(p->d_perm);
+    }
+    delete p;
+    return DCOL_SUCCESS;
+}
+
+int dcol_plan_num_launches(const dcol_plan* p, int32_t* n) {
+    if (!p || !n) return fail(DCOL_ERR_ARG, "dcol_plan_num_launches: NULL argument");
+    *n = (int32_t)p->launches.size();
+    return DCOL_SUCCESS;
+}
+
+int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, double tol, int32_t max_iter,
+                  int32_t flags, double* alpha, double* contact, double* grad, int32_t* iters, int32_t* status,
+                  void* stream) {
+    if (!p) return fail(DCOL_ERR_ARG, "dcol_plan_run: NULL plan");
+    if (p->B == 0) return DCOL_SUCCESS;
+    if (!pose1 || !pose2 || !alpha) return fail(DCOL_ERR_ARG, "dcol_plan_run: pose1, pose2 and alpha are required");
+    if ((flags & DCOL_CONTACT) && !contact) return fail(DCOL_ERR_ARG, "dcol_plan_run: DCOL_CONTACT needs contact[]");
+    if ((flags & (DCOL_GRAD_FD | DCOL_GRAD_ENVELOPE)) && !grad) return fail(DCOL_ERR_ARG, "dcol_plan_run: gradient flag needs grad[]");
+    if (max_iter < 0) return fail(DCOL_ERR_ARG, "dcol_plan_run: max_iter < 0");
+    const dcol_table* t = p->table;
+    DeviceGuard g(t->device);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    KArgs a;
+    a.shapes = t->d_shapes;
+    a.rows = t->d_rows;
+    a.s1 = p->d_s1;
+    a.s2 = p->d_s2;
+    a.pose1 = pose1;
+    a.pose2 = pose2;
+    a.perm = p->d_perm;
+    a.B = p->B;
+    a.tol = tol;
+    a.max_iter = max_iter;
+    a.flags = flags;
+    a.alpha = alpha;
+    a.contact = contact;
+    a.grad = grad;
+    a.iters = iters;
+    a.status = status;
+    for (const Launch& L : p->launches) {
+        a.slot0 = L.slot0;
+        a.n = L.n;
+        hipError_t e;
+        if (L.kind == 1) {
+            const int64_t grid = (L.n + kBlock - 1) / kBlock;
+            hipLaunchKernelGGL(reject_kernel, dim3(grid), dim3(kBlock), 0, st, a, L.code);
+            e = hipGetLastError();
+        } else {
+            e = launch_variant(L.N, L.nsoc, L.omax, a, st);
+        }
+        if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_plan_run launch: ") + hipGetErrorString(e));
+    }
+    return DCOL_SUCCESS;
+}
+
+int dcol_prox_batch_host(const dcol_table* tc, int64_t B, const int32_t* s1, const int32_t* s2, const double* pose1,
+                         const double* pose2, double tol, int32_t max_iter, int32_t flags, double* alpha,
+                         double* contact, double* grad, int32_t* iters, int32_t* status) {
+    if (!tc || B < 0) return fail(DCOL_ERR_ARG, "dcol_prox_batch_host: bad arguments");
+    if (B == 0) return DCOL_SUCCESS;
+    if (!s1 || !s2 || !pose1 || !pose2 || !alpha) return fail(DCOL_ERR_ARG, "dcol_prox_batch_host: NULL array");
+    if (B > INT32_MAX) return fail(DCOL_ERR_ARG, "dcol_prox_batch_host: B exceeds 2^31-1");
+    dcol_table* t = const_cast<dcol_table*>(tc);
+    std::lock_guard<std::mutex> lk(t->mu);
+    dcol_plan p;   // transient, device arrays are views into the table's staging buffer
+    std::vector<int32_t> perm;
+    int rc = bucket_pairs(t, B, s1, s2, &p, perm);
+    if (rc != DCOL_SUCCESS) return rc;
+    DeviceGuard g(t->device);
+    // staging: doubles pose1[6B] pose2[6B] | alpha[B] contact[3B] grad[12B] ; ints s1 s2 perm iters status
+    const size_t nin = (size_t)12 * B, nout = (size_t)16 * B;
+    const size_t bytes = (nin + nout) * sizeof(double) + 5 * (size_t)B * sizeof(int32_t);
+    if (t->stage_bytes < bytes) {
+        if (t->stage) (void)hipFree(t->stage);
+        t->stage = nullptr;
+        t->stage_bytes = 0;
+        hipError_t e = hipMalloc(&t->stage, bytes);
+        if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_prox_batch_host staging: ") + hipGetErrorString(e));
+        t->stage_bytes = bytes;
+    }
+    double* dp1 = static_cast<double*>(t->stage);
+    double* dp2 = dp1 + 6 * B;
+    double* dal = dp1 + nin;
+    double* dct = dal + B;
+    double* dgr = dct + 3 * B;
+    int32_t* ib = reinterpret_cast<int32_t*>(dp1 + nin + nout);
+    p.d_s1 = ib;
+    p.d_s2 = ib + B;
+    p.d_perm = p.launches.size() > 1 ? ib + 2 * B : nullptr;
+    int32_t* dit = ib + 3 * B;
+    int32_t* dst = ib + 4 * B;
+    // one H2D copy: [pose1 soa | pose2 soa] then [s1 | s2 | perm]
+    std::vector<double> soa(nin);
+    for (int64_t i = 0; i < B; ++i)
+        for (int q = 0; q < 6; ++q) {
+            soa[q * B + i] = pose1[6 * i + q];
+            soa[(6 + q) * B + i] = pose2[6 * i + q];
+        }
+    std::vector<int32_t> ids((size_t)3 * B);
+    std::memcpy(ids.data(), s1, sizeof(int32_t) * B);
+    std::memcpy(ids.data() + B, s2, sizeof(int32_t) * B);
+    std::memcpy(ids.data() + 2 * B, perm.data(), sizeof(int32_t) * B);
+    hipError_t e = hipMemcpy(dp1, soa.data(), sizeof(double) * nin, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(ib, ids.data(), sizeof(int32_t) * 3 * B, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_prox_batch_host H2D: ") + hipGetErrorString(e));
+    rc = dcol_plan_run(&p, dp1, dp2, tol, max_iter, flags, dal, dct, dgr, dit, dst, nullptr);
+    if (rc != DCOL_SUCCESS) return rc;
+    std::vector<double> outd(nout);
+    e = hipMemcpy(outd.data(), dal, sizeof(double) * nout, hipMemcpyDeviceToHost);   // synchronises
+    if (e == hipSuccess && iters) e = hipMemcpy(iters, dit, sizeof(int32_t) * B, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && status) e = hipMemcpy(status, dst, sizeof(int32_t) * B, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_prox_batch_host D2H: ") + hipGetErrorString(e));
+    std::memcpy(alpha, outd.data(), sizeof(double) * B);
+    if (contact && (flags & DCOL_CONTACT))
+        for (int64_t i = 0; i < B; ++i)
+            for (int q = 0; q < 3; ++q) contact[3 * i + q] = outd[(size_t)B + q * B + i];
+    if (grad && (flags & (DCOL_GRAD_FD | DCOL_GRAD_ENVELOPE)))
+        for (int64_t i = 0; i < B; ++i)
+            for (int q = 0; q < 12; ++q) grad[12 * i + q] = outd[(size_t)4 * B + q * B + i];
+    return DCOL_SUCCESS;
+}
+
+}  // extern "C"

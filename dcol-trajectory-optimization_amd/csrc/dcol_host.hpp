@@ -1,0 +1,137 @@
+// dcol_host.hpp — host-side digest of primitives and pair classification, shared by the
+// C-ABI (dcol_capi.cpp) and the test-only x86 emulator (tests/emul).
+#pragma once
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/dcol.h"
+#include "dcol_device.hpp"
+#include "dcol_variants.inc"
+
+namespace dcol_host {
+using namespace dcol;
+
+inline std::string& last_error() {
+    thread_local std::string e;
+    return e;
+}
+
+inline int fail(int code, const std::string& msg) {
+    last_error() = msg;
+    return code;
+}
+
+// sorted OMAX buckets per (N, NSOC), from the compiled variant list
+inline const std::map<std::pair<int, int>, std::vector<int>>& buckets() {
+    static const std::map<std::pair<int, int>, std::vector<int>> m = [] {
+        std::map<std::pair<int, int>, std::vector<int>> r;
+#define DCOL_ADD(NN, NS, OM) r[{NN, NS}].push_back(OM);
+        DCOL_VARIANTS(DCOL_ADD)
+#undef DCOL_ADD
+        for (auto& kv : r) std::sort(kv.second.begin(), kv.second.end());
+        return r;
+    }();
+    return m;
+}
+
+// Static digest of one primitive (misc_primitive_constructor.py:4-88 ->
+// problem_matrices.py:4-209).  Every orthant row is [Qe a, g3, ex0, ex1] with
+// h = (Qe a) . r_eff; the SOC block is generated in-kernel from (kind, R, cone_c, tanb).
+inline int digest_shape(const dcol_shape_desc& d, int32_t idx, DevShape& S, std::vector<DevRow>& rows) {
+    std::memset(&S, 0, sizeof(S));
+    S.type = d.type;
+    S.row_off = (int32_t)rows.size();
+    for (int k = 0; k < 3; ++k) S.r_off[k] = d.r_offset[k];
+    for (int k = 0; k < 9; ++k) S.Q_off[k] = d.Q_offset[k];
+    auto add = [&](double a0, double a1, double a2, double g3, double e0, double e1) {
+        DevRow r;
+        std::memset(&r, 0, sizeof(r));
+        r.a[0] = a0; r.a[1] = a1; r.a[2] = a2; r.g3 = g3; r.ex[0] = e0; r.ex[1] = e1;
+        rows.push_back(r);
+    };
+    switch (d.type) {
+        case DCOL_POLYTOPE:   // G_ort = [A Qe', -b], h = A Qe' r   (:181-209)
+            if (d.nh < 1 || !d.A || !d.b) return fail(DCOL_ERR_ARG, "shape " + std::to_string(idx) + ": polytope needs nh >= 1, A, b");
+            for (int j = 0; j < d.nh; ++j) add(d.A[3 * j], d.A[3 * j + 1], d.A[3 * j + 2], -d.b[j], 0, 0);
+            S.n_ort = d.nh;
+            S.soc_kind = SOC_NONE;
+            break;
+        case DCOL_SPHERE:     // SOC only   (:151-178)
+            S.n_ort = 0;
+            S.soc_kind = SOC_BALL;
+            S.R = d.R;
+            break;
+        case DCOL_CONE: {     // G_ort = [bx', -H/4], h = bx'r; SOC [-E Qe', -(tanb 3H/4) e0]   (:125-148)
+            const double tb = std::tan(d.beta);
+            add(1.0, 0.0, 0.0, -d.H / 4, 0, 0);
+            S.n_ort = 1;
+            S.soc_kind = SOC_CONE;
+            S.tanb = tb;
+            S.cone_c = -(tb * 3 * d.H / 4);
+            break;
+        }
+        case DCOL_CAPSULE:    // G_ort = [0 0 0 -L/2 +-1]   (:4-44)
+            add(0, 0, 0, -d.L / 2, 1.0, 0);
+            add(0, 0, 0, -d.L / 2, -1.0, 0);
+            S.n_ort = 2;
+            S.soc_kind = SOC_BALL;
+            S.R = d.R;
+            S.n_extra = 1;
+            break;
+        case DCOL_CYLINDER:   // capsule rows + [-+bx', -L/2, 0], h = -+bx'r   (:47-87)
+            add(0, 0, 0, -d.L / 2, 1.0, 0);
+            add(0, 0, 0, -d.L / 2, -1.0, 0);
+            add(-1.0, 0, 0, -d.L / 2, 0, 0);
+            add(1.0, 0, 0, -d.L / 2, 0, 0);
+            S.n_ort = 4;
+            S.soc_kind = SOC_BALL;
+            S.R = d.R;
+            S.n_extra = 1;
+            break;
+        case DCOL_POLYGON:    // G_ort = [0 0 0 -b A], h = 0; SOC with Qe[:, :2]   (:90-120)
+            if (d.nh < 1 || !d.A || !d.b) return fail(DCOL_ERR_ARG, "shape " + std::to_string(idx) + ": polygon needs nh >= 1, A, b");
+            for (int j = 0; j < d.nh; ++j) add(0, 0, 0, -d.b[j], d.A[2 * j], d.A[2 * j + 1]);
+            S.n_ort = d.nh;
+            S.soc_kind = SOC_BALL;
+            S.R = d.R;
+            S.n_extra = 2;
+            break;
+        default:
+            return fail(DCOL_ERR_ARG, "shape " + std::to_string(idx) + ": unknown type " + std::to_string(d.type));
+    }
+    return DCOL_SUCCESS;
+}
+
+struct PairClass {
+    int32_t status;   // OK / UNSUPPORTED / TOO_LARGE
+    int N, nsoc, o, omax;
+};
+
+inline PairClass classify(const DevShape& a, const DevShape& b) {
+    PairClass c{DCOL_OK, 4, 0, 0, 0};
+    if (a.n_extra > 0 && b.n_extra > 0) {   // combine_problem_matrices.py:58-67 (case 4)
+        c.status = DCOL_UNSUPPORTED;
+        return c;
+    }
+    c.N = 4 + a.n_extra + b.n_extra;
+    c.nsoc = (a.soc_kind != SOC_NONE) + (b.soc_kind != SOC_NONE);
+    c.o = a.n_ort + b.n_ort;
+    auto it = buckets().find({c.N, c.nsoc});
+    if (it == buckets().end()) {
+        c.status = DCOL_TOO_LARGE;
+        return c;
+    }
+    for (int om : it->second)
+        if (om >= std::max(c.o, 1)) {
+            c.omax = om;
+            return c;
+        }
+    c.status = DCOL_TOO_LARGE;
+    return c;
+}
+
+}  // namespace dcol_host

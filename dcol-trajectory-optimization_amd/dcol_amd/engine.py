@@ -1,0 +1,276 @@
+"""Host-side engine: shape registry + device shape table + plans + batched solves.
+
+Everything numeric happens in lib/libdcol.so (HIP kernels on the GPU).  This module only
+marshals primitives into the C-ABI (include/dcol.h) and device buffers:
+
+* host path  -> dcol_prox_batch_host (numpy in / numpy out, synchronous); used by the
+  drop-in proximity_mrp / proximity_gradient and by small batches;
+* device path -> dcol_plan_run on torch CUDA (HIP) tensors already resident in HBM,
+  asynchronous on a stream; used by the batched driver, bench.py and multi-GPU sharding.
+
+torch is only plumbing here (device memory, streams); it is imported lazily so the host
+path works without it.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from collections import OrderedDict
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .shapes import ShapeSpec, make_descs, pose_of, spec_from_object
+
+DEFAULT_TOL = 1e-6        # proximity.py:6, proximity_gradient.py:91
+DEFAULT_MAX_ITER = 50     # pdip.py:408 (literal)
+
+
+class PDIPFailure(Exception):
+    """Raised like the reference's bare Exception (pdip.py:470)."""
+
+
+def _np_ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def grad_flag(grad) -> int:
+    if grad in (None, False):
+        return 0
+    if grad in (True, "fd"):
+        return _lib.GRAD_FD
+    if grad == "envelope":
+        return _lib.GRAD_ENVELOPE
+    raise ValueError(f"grad must be None, 'fd' or 'envelope', got {grad!r}")
+
+
+def raise_for_status(status: int):
+    """Map a dcol_status to the exception the reference raises for the same failure."""
+    if status == _lib.OK:
+        return
+    if status == _lib.MAXITER:
+        raise PDIPFailure("Maximum number of iterations reached, PDIP failed")   # pdip.py:470
+    if status == _lib.UNSUPPORTED:
+        raise ValueError("Failed to combine problem matrices.")                  # combine :70
+    if status == _lib.NOT_PD:
+        raise np.linalg.LinAlgError("Matrix is not positive definite")           # pdip.py:317/:434
+    if status == _lib.NONFINITE:
+        raise ValueError("array must not contain infs or NaNs")                  # scipy check_finite
+    if status == _lib.TOO_LARGE:
+        raise ValueError("pair exceeds the engine's orthant-row capacity (32 rows)")
+    raise RuntimeError(f"unknown dcol status {status}")
+
+
+@dataclass
+class Result:
+    alpha: np.ndarray
+    contact: np.ndarray | None
+    grad: np.ndarray | None
+    iters: np.ndarray
+    status: np.ndarray
+
+
+class Table:
+    """Owning wrapper of a device shape table (dcol_table)."""
+
+    def __init__(self, specs, device: int = 0):
+        lib = _lib.load()
+        descs, keep = make_descs(specs)
+        h = ctypes.c_void_p()
+        _lib.check(lib.dcol_table_create(descs, len(specs), int(device), ctypes.byref(h)), "dcol_table_create")
+        del keep
+        self.handle = h
+        self.n = len(specs)
+        self.device = int(device)
+
+    def pair_dims(self, s1: int, s2: int):
+        m, n, ns, st = (ctypes.c_int32() for _ in range(4))
+        _lib.check(_lib.load().dcol_pair_dims(self.handle, int(s1), int(s2), ctypes.byref(m), ctypes.byref(n),
+                                              ctypes.byref(ns), ctypes.byref(st)), "dcol_pair_dims")
+        return int(m.value), int(n.value), int(ns.value), int(st.value)
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                _lib.load().dcol_table_destroy(h)
+            except Exception:  # pragma: no cover - interpreter shutdown
+                pass
+            self.handle = None
+
+
+class Plan:
+    """Owning wrapper of a dcol_plan: a fixed pairing bucketed by kernel variant."""
+
+    def __init__(self, table: Table, s1, s2):
+        lib = _lib.load()
+        self.s1 = np.ascontiguousarray(s1, dtype=np.int32)
+        self.s2 = np.ascontiguousarray(s2, dtype=np.int32)
+        if self.s1.shape != self.s2.shape or self.s1.ndim != 1:
+            raise ValueError("shape id arrays must be 1-D and of equal length")
+        self.table = table
+        self.B = int(self.s1.size)
+        h = ctypes.c_void_p()
+        _lib.check(lib.dcol_plan_create(table.handle, self.B, _np_ptr(self.s1), _np_ptr(self.s2), ctypes.byref(h)),
+                   "dcol_plan_create")
+        self.handle = h
+        n = ctypes.c_int32()
+        _lib.check(lib.dcol_plan_num_launches(h, ctypes.byref(n)), "dcol_plan_num_launches")
+        self.num_launches = int(n.value)
+
+    def run(self, pose1, pose2, tol=DEFAULT_TOL, max_iter=DEFAULT_MAX_ITER, grad="fd", contact=True,
+            out=None, stream=None):
+        """Solve on the device.  pose1/pose2: torch float64 tensors [6, B] on the table's
+        device (structure of arrays).  Returns dict of torch tensors (alpha [B],
+        contact [3, B], grad [12, B], iters [B], status [B]); asynchronous on `stream`
+        (torch stream or None = current stream)."""
+        import torch
+        B = self.B
+        dev = torch.device("cuda", self.table.device)
+        for t in (pose1, pose2):
+            if t.dtype != torch.float64 or tuple(t.shape) != (6, B) or not t.is_contiguous() or t.device != dev:
+                raise ValueError(f"poses must be contiguous float64 [6, {B}] on {dev}")
+        flags = grad_flag(grad) | (_lib.CONTACT if contact else 0)
+        if out is None:
+            out = alloc_outputs(B, dev, bool(flags & (_lib.GRAD_FD | _lib.GRAD_ENVELOPE)), bool(contact))
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        _lib.check(_lib.load().dcol_plan_run(self.handle, ptr(pose1), ptr(pose2), float(tol), int(max_iter), flags,
+                                             ptr(out["alpha"]), ptr(out.get("contact")), ptr(out.get("grad")),
+                                             ptr(out["iters"]), ptr(out["status"]), ctypes.c_void_p(stream.cuda_stream)),
+                   "dcol_plan_run")
+        return out
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                _lib.load().dcol_plan_destroy(h)
+            except Exception:  # pragma: no cover
+                pass
+            self.handle = None
+
+
+def alloc_outputs(B: int, device, want_grad=True, want_contact=True):
+    import torch
+    out = {"alpha": torch.empty(B, dtype=torch.float64, device=device),
+           "iters": torch.empty(B, dtype=torch.int32, device=device),
+           "status": torch.empty(B, dtype=torch.int32, device=device)}
+    if want_contact:
+        out["contact"] = torch.empty((3, B), dtype=torch.float64, device=device)
+    if want_grad:
+        out["grad"] = torch.empty((12, B), dtype=torch.float64, device=device)
+    return out
+
+
+class Engine:
+    """Shape registry + lazily (re)built device table.
+
+    Shapes are deduplicated by content; a primitive OBJECT's static fields are snapshotted
+    the first time it is seen (its pose .r/.p is read at every call, like the reference).
+    Call :meth:`forget` after mutating a primitive's shape parameters in place."""
+
+    def __init__(self, device: int = 0):
+        self.device = int(device)
+        self._specs: list[ShapeSpec] = []
+        self._ids: dict[ShapeSpec, int] = {}
+        self._obj_ids: dict[int, tuple[object, int]] = {}
+        self._table: Table | None = None
+        self._plans: OrderedDict = OrderedDict()
+        self._lock = threading.RLock()
+
+    # ---------------------------------------------------------------- registry
+    def register(self, spec: ShapeSpec) -> int:
+        with self._lock:
+            i = self._ids.get(spec)
+            if i is None:
+                i = len(self._specs)
+                self._specs.append(spec)
+                self._ids[spec] = i
+                self._table = None
+                self._plans.clear()
+            return i
+
+    def register_object(self, obj) -> int:
+        key = id(obj)
+        hit = self._obj_ids.get(key)
+        if hit is not None and hit[0] is obj:
+            return hit[1]
+        i = self.register(spec_from_object(obj))
+        self._obj_ids[key] = (obj, i)     # strong ref keeps id(obj) from being reused
+        return i
+
+    def forget(self, obj):
+        self._obj_ids.pop(id(obj), None)
+
+    @property
+    def table(self) -> Table:
+        with self._lock:
+            if self._table is None:
+                self._table = Table(self._specs, self.device)
+            return self._table
+
+    def plan(self, s1, s2, cache=True) -> Plan:
+        s1 = np.ascontiguousarray(s1, dtype=np.int32)
+        s2 = np.ascontiguousarray(s2, dtype=np.int32)
+        if not cache:
+            return Plan(self.table, s1, s2)
+        key = (s1.tobytes(), s2.tobytes())
+        with self._lock:
+            p = self._plans.get(key)
+            if p is None or p.table is not self.table:
+                p = Plan(self.table, s1, s2)
+                self._plans[key] = p
+                if len(self._plans) > 32:
+                    self._plans.popitem(last=False)
+            else:
+                self._plans.move_to_end(key)
+            return p
+
+    # ---------------------------------------------------------------- solves
+    def solve_host(self, s1, s2, pose1, pose2, tol=DEFAULT_TOL, max_iter=DEFAULT_MAX_ITER, grad="fd",
+                   contact=True) -> Result:
+        """Host arrays in/out: s1, s2 int [B]; pose1, pose2 float64 [B, 6] (r, p)."""
+        s1 = np.ascontiguousarray(s1, dtype=np.int32).reshape(-1)
+        s2 = np.ascontiguousarray(s2, dtype=np.int32).reshape(-1)
+        B = s1.size
+        p1 = np.ascontiguousarray(pose1, dtype=np.float64).reshape(B, 6)
+        p2 = np.ascontiguousarray(pose2, dtype=np.float64).reshape(B, 6)
+        flags = grad_flag(grad) | (_lib.CONTACT if contact else 0)
+        alpha = np.empty(B)
+        cp = np.empty((B, 3)) if contact else None
+        g = np.empty((B, 12)) if flags & (_lib.GRAD_FD | _lib.GRAD_ENVELOPE) else None
+        iters = np.empty(B, dtype=np.int32)
+        status = np.empty(B, dtype=np.int32)
+        table = self.table
+        _lib.check(_lib.load().dcol_prox_batch_host(table.handle, B, _np_ptr(s1), _np_ptr(s2), _np_ptr(p1), _np_ptr(p2),
+                                                    float(tol), int(max_iter), flags, _np_ptr(alpha), _np_ptr(cp),
+                                                    _np_ptr(g), _np_ptr(iters), _np_ptr(status)),
+                   "dcol_prox_batch_host")
+        return Result(alpha, cp, g, iters, status)
+
+    def solve_objects(self, prims1, prims2, tol=DEFAULT_TOL, max_iter=DEFAULT_MAX_ITER, grad="fd",
+                      contact=True) -> Result:
+        """Batched form of the drop-in: two equal-length sequences of primitive objects,
+        each at its current pose."""
+        s1 = np.fromiter((self.register_object(o) for o in prims1), dtype=np.int32)
+        s2 = np.fromiter((self.register_object(o) for o in prims2), dtype=np.int32)
+        if s1.size != s2.size:
+            raise ValueError("prims1 and prims2 must have equal length")
+        p1 = np.array([pose_of(o) for o in prims1]).reshape(-1, 6)
+        p2 = np.array([pose_of(o) for o in prims2]).reshape(-1, 6)
+        return self.solve_host(s1, s2, p1, p2, tol, max_iter, grad, contact)
+
+
+_default: Engine | None = None
+_default_lock = threading.Lock()
+
+
+def default_engine() -> Engine:
+    global _default
+    with _default_lock:
+        if _default is None:
+            _default = Engine(device=0)
+        return _default

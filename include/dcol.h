@@ -105,7 +105,7 @@ int dcol_pair_dims(const dcol_table* table, int32_t s1, int32_t s2, int32_t* m, 
 /* ---- plans ---------------------------------------------------------------------------
  * A plan fixes the pairing (shape ids, HOST arrays of length B) and buckets the pairs by
  * kernel variant.  It is reusable for any poses: ALTRO evaluates the same
- * (knot x obstacle) pairing at every iteration (systems/*.py inequality_constraints_x). */
+ * (knot x obstacle) pairing at every iteration (systems/<name>.py inequality_constraints_x). */
 int dcol_plan_create(const dcol_table* table, int64_t B, const int32_t* shape1,
                      const int32_t* shape2, dcol_plan** out);
 int dcol_plan_destroy(dcol_plan* plan);

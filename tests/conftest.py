@@ -1,0 +1,64 @@
+"""Shared test configuration.
+
+Markers: ``gpu`` tests need an MI355X (run on the GPU box: ``pytest -m gpu``); everything
+else runs on the CPU-only build container.  Paths: the repo root (for ``oracle``) and the
+package root ``dcol-trajectory-optimization_amd`` (for ``dcol_amd``, ``proximity``,
+``primitives``, laid out like the reference's repository root).
+"""
+import glob
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "dcol-trajectory-optimization_amd")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+for p in (PKG, REPO):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+# parity tolerances (north star: alpha 1e-6 rel, gradient 1e-5 rel; SURVEY.md §7: the
+# reference's own FD gradient is noisy at ~1e-7 of ||g||, so the gradient check is
+# norm-relative with a floor of 1, and alpha gets an absolute floor for alpha ~ 0)
+ALPHA_RTOL = 1e-6
+ALPHA_ATOL = 1e-12
+GRAD_TOL = 1e-5
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD Instinct MI355X (HIP) device")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+def golden_files():
+    return sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+
+
+def load_golden(path):
+    return dict(np.load(path, allow_pickle=False))
+
+
+def alpha_close(a, ref):
+    return np.abs(a - ref) <= ALPHA_RTOL * np.abs(ref) + ALPHA_ATOL
+
+
+def grad_close(g, ref):
+    return np.abs(g - ref).max(axis=-1) <= GRAD_TOL * np.maximum(np.abs(ref).max(axis=-1), 1.0)
+
+
+def gpu_available():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def engine():
+    if not gpu_available():
+        pytest.skip("no GPU")
+    from dcol_amd import Engine
+    return Engine(device=0)
