@@ -83,7 +83,7 @@ struct dcol_table {
 
 struct Launch {
     int kind;       // 0 = solve, 1 = reject
-    int N, nsoc, omax;
+    int N, nsoc, omax, lpp;
     int32_t code;   // reject status
     int64_t slot0, n;
 };
@@ -100,11 +100,10 @@ struct dcol_plan {
 
 namespace {
 
-hipError_t launch_variant(int N, int nsoc, int omax, const KArgs& a, hipStream_t st) {
-    const int64_t grid = (a.n + kBlock - 1) / kBlock;
-    if (N == 4) return launch_n4(nsoc, omax, a, grid, st);
-    if (N == 5) return launch_n5(nsoc, omax, a, grid, st);
-    if (N == 6) return launch_n6(nsoc, omax, a, grid, st);
+hipError_t launch_variant(int N, int nsoc, int omax, int lpp, const KArgs& a, hipStream_t st) {
+    if (N == 4) return launch_n4(nsoc, omax, lpp, a, st);
+    if (N == 5) return launch_n5(nsoc, omax, lpp, a, st);
+    if (N == 6) return launch_n6(nsoc, omax, lpp, a, st);
     return hipErrorInvalidValue;
 }
 
@@ -208,13 +207,13 @@ namespace {
 int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, dcol_plan* p,
                  std::vector<int32_t>& perm) {
     const int32_t ns = (int32_t)t->shapes.size();
-    using Key = std::tuple<int, int, int, int, int>;   // kind, N, nsoc, omax, code
+    using Key = std::tuple<int, int, int, int, int, int>;   // kind, N, nsoc, omax, lpp, code
     std::map<Key, std::vector<int32_t>> groups;
     for (int64_t i = 0; i < B; ++i) {
         if (s1[i] < 0 || s1[i] >= ns || s2[i] < 0 || s2[i] >= ns)
             return fail(DCOL_ERR_ARG, "shape id out of range at pair " + std::to_string(i));
         PairClass c = classify(t->shapes[s1[i]], t->shapes[s2[i]]);
-        Key k = c.status == DCOL_OK ? Key{0, c.N, c.nsoc, c.omax, 0} : Key{1, 0, 0, 0, c.status};
+        Key k = c.status == DCOL_OK ? Key{0, c.N, c.nsoc, c.omax, c.lpp, 0} : Key{1, 0, 0, 0, 0, c.status};
         groups[k].push_back((int32_t)i);
     }
     p->table = t;
@@ -228,7 +227,8 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
         L.N = std::get<1>(kv.first);
         L.nsoc = std::get<2>(kv.first);
         L.omax = std::get<3>(kv.first);
-        L.code = std::get<4>(kv.first);
+        L.lpp = std::get<4>(kv.first);
+        L.code = std::get<5>(kv.first);
         L.slot0 = (int64_t)perm.size();
         L.n = (int64_t)kv.second.size();
         perm.insert(perm.end(), kv.second.begin(), kv.second.end());
@@ -330,7 +330,7 @@ int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, 
             hipLaunchKernelGGL(reject_kernel, dim3(grid), dim3(kBlock), 0, st, a, L.code);
             e = hipGetLastError();
         } else {
-            e = launch_variant(L.N, L.nsoc, L.omax, a, st);
+            e = launch_variant(L.N, L.nsoc, L.omax, L.lpp, a, st);
         }
         if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_plan_run launch: ") + hipGetErrorString(e));
     }

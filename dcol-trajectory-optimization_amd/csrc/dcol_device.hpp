@@ -258,29 +258,101 @@ DCOL_HD double soc_ls(const double* y, const double* d) {
 }
 
 // ------------------------------------------------------------------------------------
+// lane-group reductions (one pair = LPP consecutive lanes; DPP quad permutations)
+// ------------------------------------------------------------------------------------
+// Butterflies with commutative adds: every lane of a group ends with the bitwise same
+// value, so the replicated scalar part of the method (Cholesky, mu, sigma, step) takes
+// identical decisions in every lane of the pair.
+#if defined(__HIP_DEVICE_COMPILE__)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    int lo = (int)(b & 0xffffffffLL), hi = (int)(b >> 32);
+    lo = __builtin_amdgcn_mov_dpp(lo, CTRL, 0xF, 0xF, false);
+    hi = __builtin_amdgcn_mov_dpp(hi, CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+#define DCOL_XOR1(v) dpp_d<0xB1>(v)   // quad_perm [1,0,3,2]
+#define DCOL_XOR2(v) dpp_d<0x4E>(v)   // quad_perm [2,3,0,1]
+#else
+#define DCOL_XOR1(v) (__builtin_trap(), (v))   // multi-lane groups run on the GPU only
+#define DCOL_XOR2(v) (__builtin_trap(), (v))
+#endif
+
+template <int LPP>
+struct Grp;
+template <>
+struct Grp<1> {
+    DCOL_HD static double sum(double v) { return v; }
+    DCOL_HD static double min(double v) { return v; }
+    DCOL_HD static double max(double v) { return v; }
+};
+template <>
+struct Grp<2> {
+    DCOL_HD static double sum(double v) { return v + DCOL_XOR1(v); }
+    DCOL_HD static double min(double v) { return fmin(v, DCOL_XOR1(v)); }
+    DCOL_HD static double max(double v) { return fmax(v, DCOL_XOR1(v)); }
+};
+template <>
+struct Grp<4> {
+    DCOL_HD static double sum(double v) {
+        v = v + DCOL_XOR1(v);
+        return v + DCOL_XOR2(v);
+    }
+    DCOL_HD static double min(double v) {
+        v = fmin(v, DCOL_XOR1(v));
+        return fmin(v, DCOL_XOR2(v));
+    }
+    DCOL_HD static double max(double v) {
+        v = fmax(v, DCOL_XOR1(v));
+        return fmax(v, DCOL_XOR2(v));
+    }
+};
+
+// ------------------------------------------------------------------------------------
 // the per-pair solver
 // ------------------------------------------------------------------------------------
-template <int N, int NSOC, int OMAX>
+// A pair's rows are spread over LPP lanes: orthant row i lives in lane i % LPP, slot
+// i / LPP; SOC block b lives in lane b % LPP, SOC slot b / LPP.  Per-row work is lane
+// local; sums over rows are group all-reduces; the n x n part (normal matrix Cholesky and
+// triangular solves, step lengths) is replicated in every lane of the group.
+//
+// Rounding-level reformulations relative to the reference (none changes the algorithm):
+//  * orthant NT scaling from lambda = sqrt(s z): w = s/lambda, w^-1 = z/lambda and
+//    lambda\v = v/lambda share ONE reciprocal per row per iteration;
+//    lambda o lambda = s z;
+//  * the primal residual r = G x - h is carried incrementally (r += a G dx);
+//  * the orthant ratio test keeps the argmin by cross-multiplication and divides once;
+//  * G~ = W^-1 G is never formed: G~'G~ and G~'v accumulate G'(W^-1 ...).
+template <int N, int NSOC, int OMAX, int LPP>
 struct Solver {
-    static constexpr int M = OMAX + 4 * NSOC;
-    static constexpr int NH = N * (N + 1) / 2;
+    static_assert(OMAX % LPP == 0, "OMAX must be a multiple of LPP");
+    static constexpr int OR = OMAX / LPP;              // orthant slots per lane
+    static constexpr int SS = (NSOC + LPP - 1) / LPP;  // SOC slots per lane
+    static constexpr int M = OR + 4 * SS;              // lane-local rows
+    static constexpr int SSA = SS > 0 ? SS : 1;
+    using R = Grp<LPP>;
 
-    // state
     double G[M][N];
-    double h[M];
-    double x[N], s[M], z[M];
-    int o1, o;
+    double s[M], z[M], r[M];   // slack, dual, primal residual G x - h
+    double x[N];
+    int q, o1, o, deg;
+    bool vs[SSA];              // SOC slot holds a real block
+    int soc_owner[SSA];        // primitive (0/1) owning the block in SOC slot b
 
-    DCOL_HD static bool valid(int i, int o_) { return i >= OMAX || i < o_; }
+    DCOL_HD bool vort(int k) const { return k * LPP + q < o; }
+    DCOL_HD bool vrow(int k) const { return k < OR ? vort(k) : vs[(k - OR) / 4]; }
 
     // -------- assembly (problem_matrices.py + combine_problem_matrices.py) --------------
-    DCOL_HD void assemble(const KArgs& A, const DevShape& S1, const DevShape& S2,
-                                             const Frame& F1, const Frame& F2, int slot_owner[2]) {
+    // leaves h in r[] (init turns it into G x_hat - h)
+    DCOL_HD void assemble(const KArgs& A, const DevShape& S1, const DevShape& S2, const Frame& F1, const Frame& F2) {
         o1 = S1.n_ort;
         o = o1 + S2.n_ort;
+        deg = o + NSOC;                                   // quirk Q7
         const double* __restrict__ rows = reinterpret_cast<const double*>(A.rows);
 #pragma unroll
-        for (int i = 0; i < OMAX; ++i) {
+        for (int k = 0; k < OR; ++k) {
+            const int i = k * LPP + q;
             const bool v = i < o;
             const bool p2 = i >= o1;
             double a0 = 0, a1 = 0, a2 = 0, g3 = 0, e0 = 0, e1 = 0;
@@ -292,42 +364,42 @@ struct Solver {
             }
             double Qe[9], re[3];
 #pragma unroll
-            for (int k = 0; k < 9; ++k) Qe[k] = p2 ? F2.Qe[k] : F1.Qe[k];
+            for (int c = 0; c < 9; ++c) Qe[c] = p2 ? F2.Qe[c] : F1.Qe[c];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) re[k] = p2 ? F2.re[k] : F1.re[k];
+            for (int c = 0; c < 3; ++c) re[c] = p2 ? F2.re[c] : F1.re[c];
             const double u0 = Qe[0] * a0 + Qe[1] * a1 + Qe[2] * a2;
             const double u1 = Qe[3] * a0 + Qe[4] * a1 + Qe[5] * a2;
             const double u2 = Qe[6] * a0 + Qe[7] * a1 + Qe[8] * a2;
-            G[i][0] = u0; G[i][1] = u1; G[i][2] = u2; G[i][3] = g3;
-            if constexpr (N > 4) G[i][4] = e0;
-            if constexpr (N > 5) G[i][5] = e1;
-            h[i] = u0 * re[0] + u1 * re[1] + u2 * re[2];
+            G[k][0] = u0; G[k][1] = u1; G[k][2] = u2; G[k][3] = g3;
+            if constexpr (N > 4) G[k][4] = e0;
+            if constexpr (N > 5) G[k][5] = e1;
+            r[k] = u0 * re[0] + u1 * re[1] + u2 * re[2];
         }
-        // SOC blocks: slot 0 = first primitive with a SOC, slot 1 = prim 2 when both have one
-        slot_owner[0] = S1.soc_kind != SOC_NONE ? 0 : 1;
-        slot_owner[1] = 1;
+        // global SOC block 0 = first primitive with a SOC, block 1 = prim 2 when both have one
+        const int own0 = S1.soc_kind != SOC_NONE ? 0 : 1;
 #pragma unroll
-        for (int b = 0; b < NSOC; ++b) {
-            const bool p2 = slot_owner[b] == 1;
-            const int kind = p2 ? S2.soc_kind : S1.soc_kind;
-            const double R = p2 ? S2.R : S1.R;
-            const double cc = p2 ? S2.cone_c : S1.cone_c;
-            const double tb = p2 ? S2.tanb : S1.tanb;
-            const int nx = p2 ? S2.n_extra : S1.n_extra;
+        for (int b = 0; b < SS; ++b) {
+            const int gb = b * LPP + q;
+            vs[b] = gb < NSOC;
+            const bool p2 = (gb == 0) ? (own0 == 1) : true;
+            soc_owner[b] = p2 ? 1 : 0;
             double Qe[9], re[3];
 #pragma unroll
-            for (int k = 0; k < 9; ++k) Qe[k] = p2 ? F2.Qe[k] : F1.Qe[k];
+            for (int c = 0; c < 9; ++c) Qe[c] = p2 ? F2.Qe[c] : F1.Qe[c];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) re[k] = p2 ? F2.re[k] : F1.re[k];
-            soc_rows(kind, R, cc, tb, nx, Qe, re, &G[OMAX + 4 * b], &h[OMAX + 4 * b]);
+            for (int c = 0; c < 3; ++c) re[c] = p2 ? F2.re[c] : F1.re[c];
+            const int kind = vs[b] ? (p2 ? S2.soc_kind : S1.soc_kind) : SOC_NONE;
+            soc_rows(kind, p2 ? S2.R : S1.R, p2 ? S2.cone_c : S1.cone_c, p2 ? S2.tanb : S1.tanb,
+                     p2 ? S2.n_extra : S1.n_extra, Qe, re, &G[OR + 4 * b], &r[OR + 4 * b]);
         }
     }
 
-    // The 4 rows of one SOC block.  Ball (sphere/capsule/cylinder/polygon):
-    //   [0 0 0 -R | 0..], h 0;  [-e_k | 0 | Qe[k][0..nx)], h -re[k]     (problem_matrices.py:21-28, 66-76, 112-119, 165-176)
-    // Cone: [-E Qe' | -(tanb 3H/4) e_0], h = -E Qe' re; 4th row zero     (problem_matrices.py:138-145)
-    DCOL_HD static void soc_rows(int kind, double R, double cc, double tb, int nx,
-                                                    const double* Qe, const double* re, double (*Gb)[N], double* hb) {
+    // The 4 rows of one SOC block (kind SOC_NONE -> inert zero block).  Ball (sphere/
+    // capsule/cylinder/polygon): [0 0 0 -R | 0..], h 0;  [-e_k | 0 | Qe[k][0..nx)], h -re[k]
+    //   (problem_matrices.py:21-28, 66-76, 112-119, 165-176)
+    // Cone: [-E Qe' | -(tanb 3H/4) e_0], h = -E Qe' re; 4th row zero  (problem_matrices.py:138-145)
+    DCOL_HD static void soc_rows(int kind, double R, double cc, double tb, int nx, const double* Qe,
+                                 const double* re, double (*Gb)[N], double* hb) {
         if (kind == SOC_CONE) {
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
@@ -344,7 +416,7 @@ struct Solver {
 #pragma unroll
             for (int j = 0; j < N; ++j) Gb[3][j] = 0.0;
             hb[3] = 0.0;
-        } else {
+        } else if (kind == SOC_BALL) {
             Gb[0][0] = 0.0; Gb[0][1] = 0.0; Gb[0][2] = 0.0; Gb[0][3] = -R;
 #pragma unroll
             for (int j = 4; j < N; ++j) Gb[0][j] = 0.0;
@@ -358,33 +430,25 @@ struct Solver {
                 if constexpr (N > 5) Gb[k + 1][5] = (nx >= 2) ? Qe[3 * k + 1] : 0.0;
                 hb[k + 1] = -re[k];
             }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+#pragma unroll
+                for (int j = 0; j < N; ++j) Gb[k][j] = 0.0;
+                hb[k] = 0.0;
+            }
         }
     }
 
     // -------- small dense helpers ------------------------------------------------------
-    // y = G x - h (per row, pads -> 0 since G = h = 0)
-    DCOL_HD void Gx(const double* v, double* out) const {
+    DCOL_HD double rowdot(int k, const double* v) const {
+        double acc = G[k][0] * v[0];
 #pragma unroll
-        for (int i = 0; i < M; ++i) {
-            double acc = G[i][0] * v[0];
-#pragma unroll
-            for (int j = 1; j < N; ++j) acc += G[i][j] * v[j];
-            out[i] = acc;
-        }
+        for (int j = 1; j < N; ++j) acc += G[k][j] * v[j];
+        return acc;
     }
-    // out = G' w   (pads contribute 0 * w = 0: w is finite on pads)
-    DCOL_HD void GTx(const double* w, double* out) const {
-#pragma unroll
-        for (int j = 0; j < N; ++j) out[j] = 0.0;
-#pragma unroll
-        for (int i = 0; i < M; ++i)
-#pragma unroll
-            for (int j = 0; j < N; ++j) out[j] += G[i][j] * w[i];
-    }
-
-    // upper Cholesky H = F'F on packed upper triangle (scipy.linalg.cholesky semantics);
-    // returns false if a pivot is <= 0 or NaN (LAPACK dpotrf info > 0)
-    DCOL_HD static bool chol(double (&H)[N][N], double (&F)[N][N], double (&idg)[N]) {
+    // upper Cholesky H = F'F (scipy.linalg.cholesky); false if a pivot is <= 0 or NaN
+    DCOL_HD static bool chol(const double (&H)[N][N], double (&F)[N][N], double (&idg)[N]) {
         bool ok = true;
 #pragma unroll
         for (int j = 0; j < N; ++j) {
@@ -423,272 +487,245 @@ struct Solver {
             out[j] = t * idg[j];
         }
     }
-
-    // bring2cone, pdip.py:237-287 (quirk Q11)
-    DCOL_HD void bring2cone(double* r) const {
-        double a = -1.0;
-        bool any = false;
-        double mn = 0.0;
+    // group all-reduce of the packed upper triangle / of an N-vector
+    DCOL_HD static void allsum_sym(double (&H)[N][N]) {
 #pragma unroll
-        for (int i = 0; i < OMAX; ++i) {
-            if (i < o) {
-                if (r[i] <= 0.0) any = true;
-                mn = (i == 0) ? r[i] : fmin(mn, r[i]);
+        for (int j = 0; j < N; ++j)
+#pragma unroll
+            for (int c = j; c < N; ++c) H[j][c] = R::sum(H[j][c]);
+    }
+    DCOL_HD static void allsum_vec(double* v) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) v[j] = R::sum(v[j]);
+    }
+
+    // bring2cone, pdip.py:237-287 (quirk Q11), group-wide
+    DCOL_HD void bring2cone(double* v) const {
+        double any = 0.0, mn = __builtin_inf(), socv = -__builtin_inf();
+#pragma unroll
+        for (int k = 0; k < OR; ++k) {
+            if (vort(k)) {
+                if (v[k] <= 0.0) any = 1.0;
+                mn = fmin(mn, v[k]);
             }
         }
-        if (any) a = -mn;
 #pragma unroll
-        for (int b = 0; b < NSOC; ++b) {
-            const double* q = r + OMAX + 4 * b;
-            const double res = q[0] - sqrt(q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-            if (res <= 0.0) a = fmax(a, -res);
+        for (int b = 0; b < SS; ++b) {
+            if (vs[b]) {
+                const double* p = v + OR + 4 * b;
+                const double res = p[0] - sqrt(p[1] * p[1] + p[2] * p[2] + p[3] * p[3]);
+                if (res <= 0.0) socv = fmax(socv, -res);
+            }
         }
+        any = R::max(any);
+        mn = R::min(mn);
+        socv = R::max(socv);
+        double a = -1.0;
+        if (any > 0.0) a = -mn;
+        a = fmax(a, socv);
         if (a >= 0.0) {
             const double sh = 1.0 + a;
 #pragma unroll
-            for (int i = 0; i < OMAX; ++i)
-                if (i < o) r[i] += sh;
+            for (int k = 0; k < OR; ++k)
+                if (vort(k)) v[k] += sh;
 #pragma unroll
-            for (int b = 0; b < NSOC; ++b) r[OMAX + 4 * b] += sh;
+            for (int b = 0; b < SS; ++b)
+                if (vs[b]) v[OR + 4 * b] += sh;
         }
     }
 
     // -------- initialize, pdip.py:291-332 ------------------------------------------------
     DCOL_HD bool initialize() {
-        double H[N][N], F[N][N], idg[N];
+        double H[N][N], F[N][N], idg[N], gth[N];
 #pragma unroll
-        for (int j = 0; j < N; ++j)
+        for (int j = 0; j < N; ++j) {
+            gth[j] = 0.0;
 #pragma unroll
-            for (int c = j; c < N; ++c) {
-                double acc = 0.0;
+            for (int c = j; c < N; ++c) H[j][c] = 0.0;
+        }
 #pragma unroll
-                for (int i = 0; i < M; ++i) acc += G[i][j] * G[i][c];
-                H[j][c] = acc;
+        for (int k = 0; k < M; ++k) {
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                gth[j] += G[k][j] * r[k];          // r holds h here
+#pragma unroll
+                for (int c = j; c < N; ++c) H[j][c] += G[k][j] * G[k][c];
             }
-        const bool ok = chol(H, F, idg);   // F' = np.linalg.cholesky(G'G) (lower L = F')
-        double gth[N], xh[N];
-        GTx(h, gth);
-        chol_solve(F, idg, gth, xh);        // x_hat = L^-T L^-1 G'h
-        double r[M];
-        Gx(xh, r);
+        }
+        allsum_sym(H);
+        allsum_vec(gth);
+        const bool ok = chol(H, F, idg);             // F' = np.linalg.cholesky(G'G)
+        chol_solve(F, idg, gth, x);                  // x_hat = L^-T L^-1 G'h
+        double t[M];
 #pragma unroll
-        for (int i = 0; i < M; ++i) r[i] -= h[i];   // quirk Q2: G x_hat - h
-        bring2cone(r);
+        for (int k = 0; k < M; ++k) {
+            r[k] = rowdot(k, x) - r[k];              // r = G x_hat - h  (quirk Q2: s~ = G x_hat - h)
+            t[k] = r[k];
+        }
+        bring2cone(t);
         // quirk Q1: y = solve_triangular(L, -c) with lower=False reads diag(L) only:
-        // y = -c / diag(L) = -e_3 / L_33;  then x = L^-T y (proper back substitution)
-        double yv[N], xz[N];
-#pragma unroll
-        for (int j = 0; j < N; ++j) yv[j] = (j == 3) ? -idg[3] : 0.0;
+        // y = -e_3 / L_33, then x = L^-T y
+        double xz[N];
 #pragma unroll
         for (int j = N - 1; j >= 0; --j) {
-            double t = yv[j];
+            double acc = (j == 3) ? -idg[3] : 0.0;
 #pragma unroll
-            for (int k = j + 1; k < N; ++k) t -= F[j][k] * xz[k];
-            xz[j] = t * idg[j];
+            for (int k = j + 1; k < N; ++k) acc -= F[j][k] * xz[k];
+            xz[j] = acc * idg[j];
         }
         double zt[M];
-        Gx(xz, zt);
+#pragma unroll
+        for (int k = 0; k < M; ++k) zt[k] = rowdot(k, xz);
         bring2cone(zt);
 #pragma unroll
-        for (int j = 0; j < N; ++j) x[j] = xh[j];
-#pragma unroll
-        for (int i = 0; i < M; ++i) {
-            const bool v = valid(i, o);
-            s[i] = v ? r[i] : 1.0;
-            z[i] = v ? zt[i] : 1.0;
+        for (int k = 0; k < M; ++k) {
+            const bool v = vrow(k);
+            const double one = (k < OR || ((k - OR) & 3) == 0) ? 1.0 : 0.0;   // inert: e
+            s[k] = v ? t[k] : one;
+            z[k] = v ? zt[k] : one;
         }
         return ok;
     }
 
-    // -------- NT scaling application ---------------------------------------------------
-    struct Scaling {
-        double w[OMAX], wi[OMAX];
-        SocNT soc[NSOC > 0 ? NSOC : 1];
-    };
-    DCOL_HD static void mulW(const Scaling& W, const double* v, double* out) {
-#pragma unroll
-        for (int i = 0; i < OMAX; ++i) out[i] = v[i] * W.w[i];
-#pragma unroll
-        for (int b = 0; b < NSOC; ++b) soc_mul(W.soc[b], v + OMAX + 4 * b, out + OMAX + 4 * b);
-    }
-    DCOL_HD static void solveW(const Scaling& W, const double* v, double* out) {
-#pragma unroll
-        for (int i = 0; i < OMAX; ++i) out[i] = v[i] * W.wi[i];
-#pragma unroll
-        for (int b = 0; b < NSOC; ++b) soc_solve(W.soc[b], v + OMAX + 4 * b, out + OMAX + 4 * b);
-    }
-    DCOL_HD static void cone_prod(const double* u, const double* v, double* out) {
-#pragma unroll
-        for (int i = 0; i < OMAX; ++i) out[i] = u[i] * v[i];
-#pragma unroll
-        for (int b = 0; b < NSOC; ++b) soc_prod(u + OMAX + 4 * b, v + OMAX + 4 * b, out + OMAX + 4 * b);
-    }
-    DCOL_HD static void cone_iprod(const double* lam, const double* v, double* out) {
-#pragma unroll
-        for (int i = 0; i < OMAX; ++i) out[i] = v[i] / lam[i];
-#pragma unroll
-        for (int b = 0; b < NSOC; ++b) soc_iprod(lam + OMAX + 4 * b, v + OMAX + 4 * b, out + OMAX + 4 * b);
-    }
-    // linesearch, pdip.py:55-85
-    DCOL_HD double linesearch(const double* v, const double* d) const {
-        double a = 1.0;
-#pragma unroll
-        for (int i = 0; i < OMAX; ++i)
-            if (i < o && d[i] < 0.0) a = fmin(a, -v[i] / d[i]);
-#pragma unroll
-        for (int b = 0; b < NSOC; ++b) a = fmin(a, soc_ls(v + OMAX + 4 * b, d + OMAX + 4 * b));
-        return a;
-    }
-    DCOL_HD double dotm(const double* u, const double* v) const {
-        double acc = 0.0;
-#pragma unroll
-        for (int i = 0; i < M; ++i)
-            if (valid(i, o)) acc += u[i] * v[i];
-        return acc;
+    // line-search candidate: keep argmin of x / (-d) over d < 0 by cross-multiplication
+    DCOL_HD static void ratio(double xv, double d, double& bn, double& bd) {
+        if (d < 0.0) {
+            const double nd = -d;
+            if (xv * bd < bn * nd) { bn = xv; bd = nd; }
+        }
     }
 
-    // Newton direction for a given lambda\ds:  b~z = W^-1(-rz - W lds);
-    // dx = (G~'G~)^-1 (-rx + G~' b~z); dz = W^-1(G~ dx - b~z); ds = W(lds - W dz)
-    DCOL_HD void direction(const Scaling& W, const double (&F)[N][N], const double (&idg)[N],
-                                              const double* rx, const double* rz, const double* lds,
-                                              double* dx, double* dz, double* ds) const {
-        double t[M], bzt[M];
-        mulW(W, lds, t);
-#pragma unroll
-        for (int i = 0; i < M; ++i) t[i] = -rz[i] - t[i];
-        solveW(W, t, bzt);
-        solveW(W, bzt, t);                       // t = W^-1 b~z  (G~'b~z = G' W^-1 b~z)
-        double rhs[N];
-        GTx(t, rhs);
-#pragma unroll
-        for (int j = 0; j < N; ++j) rhs[j] -= rx[j];
-        chol_solve(F, idg, rhs, dx);
-        double u[M];
-        Gx(dx, u);
-        solveW(W, u, t);                         // G~ dx = W^-1 G dx
-#pragma unroll
-        for (int i = 0; i < M; ++i) t[i] -= bzt[i];
-        solveW(W, t, dz);
-        mulW(W, dz, t);
-#pragma unroll
-        for (int i = 0; i < M; ++i) t[i] = lds[i] - t[i];
-        mulW(W, t, ds);
-    }
+    struct SocState {
+        SocNT W;
+        double lam[4];
+        double ll[4];
+    };
 
     // -------- solve_lp_pdip, pdip.py:373-470 -------------------------------------------
-    // returns status; *it = Newton steps taken
     DCOL_HD int32_t pdip(double tol, int max_iter, int* it_out) {
-        const int deg = o + NSOC;                       // quirk Q7
         int it = 0;
         int32_t st = ST_MAXITER;
         for (it = 0; it < max_iter; ++it) {
-            Scaling W;
+            // ---- NT scalings, residuals, normal matrix (pdip.py:410-434)
+            double il[OR > 0 ? OR : 1];
+            SocState so[SSA];
+            double sz = 0.0, rx[N], Hm[N][N];
 #pragma unroll
-            for (int i = 0; i < OMAX; ++i) {
-                const double wv = sqrt(s[i] / z[i]);
-                W.w[i] = wv;
-                W.wi[i] = 1.0 / wv;
-            }
-#pragma unroll
-            for (int b = 0; b < NSOC; ++b) soc_nt(s + OMAX + 4 * b, z + OMAX + 4 * b, W.soc[b]);
-            double lam[M], ll[M];
-            mulW(W, z, lam);
-            cone_prod(lam, lam, ll);
-            double rx[N], rz[M];
-            GTx(z, rx);
-            rx[3] += 1.0;                               // + c (c = e_3)
-            Gx(x, rz);
-#pragma unroll
-            for (int i = 0; i < M; ++i) rz[i] = s[i] + rz[i] - h[i];
-            const double sz = dotm(s, z);
-            const double mu = sz / (double)deg;
-            if (mu < tol) {                             // quirk Q3
-                st = ST_OK;
-                break;
-            }
-            // normal matrix G~'G~, G~ = W^-1 G  (pdip.py:429-434)
-            double Hm[N][N];
-#pragma unroll
-            for (int j = 0; j < N; ++j)
+            for (int j = 0; j < N; ++j) {
+                rx[j] = 0.0;
 #pragma unroll
                 for (int c = j; c < N; ++c) Hm[j][c] = 0.0;
+            }
 #pragma unroll
-            for (int i = 0; i < OMAX; ++i) {
+            for (int k = 0; k < OR; ++k) {
+                const double sk = s[k], zk = z[k];
+                const double lam = sqrt(sk * zk);
+                il[k] = 1.0 / lam;
+                if (vort(k)) sz += sk * zk;
+                const double wi = zk * il[k];
                 double g[N];
 #pragma unroll
-                for (int j = 0; j < N; ++j) g[j] = G[i][j] * W.wi[i];
+                for (int j = 0; j < N; ++j) {
+                    rx[j] += G[k][j] * zk;
+                    g[j] = G[k][j] * wi;
+                }
 #pragma unroll
                 for (int j = 0; j < N; ++j)
 #pragma unroll
                     for (int c = j; c < N; ++c) Hm[j][c] += g[j] * g[c];
             }
 #pragma unroll
-            for (int b = 0; b < NSOC; ++b) {
+            for (int b = 0; b < SS; ++b) {
+                const int k0 = OR + 4 * b;
+                soc_nt(s + k0, z + k0, so[b].W);
+                soc_mul(so[b].W, z + k0, so[b].lam);
+                soc_prod(so[b].lam, so[b].lam, so[b].ll);
+                if (vs[b]) sz += s[k0] * z[k0] + s[k0 + 1] * z[k0 + 1] + s[k0 + 2] * z[k0 + 2] + s[k0 + 3] * z[k0 + 3];
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int j = 0; j < N; ++j) rx[j] += G[k0 + e][j] * z[k0 + e];
+            }
+            // SOC part of the normal matrix
+#pragma unroll
+            for (int b = 0; b < SS; ++b) {
+                const int k0 = OR + 4 * b;
                 double gt[4][N];
 #pragma unroll
                 for (int j = 0; j < N; ++j) {
                     double col[4], res[4];
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) col[k] = G[OMAX + 4 * b + k][j];
-                    soc_solve(W.soc[b], col, res);
+                    for (int e = 0; e < 4; ++e) col[e] = G[k0 + e][j];
+                    soc_solve(so[b].W, col, res);
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) gt[k][j] = res[k];
+                    for (int e = 0; e < 4; ++e) gt[e][j] = res[e];
                 }
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
+                for (int e = 0; e < 4; ++e)
 #pragma unroll
                     for (int j = 0; j < N; ++j)
 #pragma unroll
-                        for (int c = j; c < N; ++c) Hm[j][c] += gt[k][j] * gt[k][c];
+                        for (int c = j; c < N; ++c) Hm[j][c] += gt[e][j] * gt[e][c];
+            }
+            sz = R::sum(sz);
+            allsum_vec(rx);
+            allsum_sym(Hm);
+            rx[3] += 1.0;                                   // + c (c = e_3)
+            const double mu = sz / (double)deg;
+            if (mu < tol) {                                 // quirk Q3
+                st = ST_OK;
+                break;
             }
             bool finite = true;
 #pragma unroll
             for (int j = 0; j < N; ++j)
 #pragma unroll
                 for (int c = j; c < N; ++c) finite = finite && __builtin_isfinite(Hm[j][c]);
-            if (!finite) { st = ST_NONFINITE; break; }  // scipy check_finite -> ValueError
+            if (!finite) { st = ST_NONFINITE; break; }       // scipy check_finite -> ValueError
             double F[N][N], idg[N];
             if (!chol(Hm, F, idg)) { st = ST_NOT_PD; break; }
 
-            // predictor (affine) step
-            double neg[M], lds[M], dx[N], dz[M], ds[M];
+            // ---- predictor (affine) direction
+            double dsA[M], dzA[M];
+            double dx[N];
+            direction(so, il, F, idg, rx, nullptr, 0.0, dx, dsA, dzA, nullptr);
+            double bn = 1.0, bd = 1.0, als = 1.0;
+            step_bound(so, dsA, dzA, bn, bd, als);
+            const double aa = R::min(fmin(bn / bd, als));           // quirk Q5 (no 0.99)
+            double rho = 0.0;
 #pragma unroll
-            for (int i = 0; i < M; ++i) neg[i] = -ll[i];
-            cone_iprod(lam, neg, lds);
-            direction(W, F, idg, rx, rz, lds, dx, dz, ds);
-            const double aa = fmin(linesearch(s, ds), linesearch(z, dz));   // quirk Q5
-            double sp[M], zp[M];
-#pragma unroll
-            for (int i = 0; i < M; ++i) {
-                sp[i] = s[i] + aa * ds[i];
-                zp[i] = z[i] + aa * dz[i];
-            }
-            const double rho = dotm(sp, zp) / sz;
+            for (int k = 0; k < M; ++k)
+                if (vrow(k)) rho += (s[k] + aa * dsA[k]) * (z[k] + aa * dzA[k]);
+            rho = R::sum(rho) / sz;
             const double sc = fmax(0.0, fmin(1.0, rho));
-            const double sigma = sc * sc * sc;         // quirk Q6
+            const double sigma = sc * sc * sc;                      // quirk Q6
+            // cp = (W^-1 ds_a) o (W dz_a)
+            double cp[M];
+#pragma unroll
+            for (int k = 0; k < OR; ++k) cp[k] = (z[k] * il[k] * dsA[k]) * (s[k] * il[k] * dzA[k]);
+#pragma unroll
+            for (int b = 0; b < SS; ++b) {
+                const int k0 = OR + 4 * b;
+                double t1[4], t2[4];
+                soc_solve(so[b].W, dsA + k0, t1);
+                soc_mul(so[b].W, dzA + k0, t2);
+                soc_prod(t1, t2, cp + k0);
+            }
 
-            // corrector (combined) step
-            double t1[M], t2[M], cp[M];
-            solveW(W, ds, t1);
-            mulW(W, dz, t2);
-            cone_prod(t1, t2, cp);
-            const double smu = sigma * mu;
-#pragma unroll
-            for (int i = 0; i < M; ++i) neg[i] = -ll[i] - cp[i];
-#pragma unroll
-            for (int i = 0; i < OMAX; ++i) neg[i] += smu;
-#pragma unroll
-            for (int b = 0; b < NSOC; ++b) neg[OMAX + 4 * b] += smu;
-            cone_iprod(lam, neg, lds);
-            direction(W, F, idg, rx, rz, lds, dx, dz, ds);
-            const double a = fmin(1.0, 0.99 * fmin(linesearch(s, ds), linesearch(z, dz)));
+            // ---- corrector (combined) direction
+            double ds[M], dz[M], u[M];
+            direction(so, il, F, idg, rx, cp, sigma * mu, dx, ds, dz, u);
+            bn = 1.0; bd = 1.0; als = 1.0;
+            step_bound(so, ds, dz, bn, bd, als);
+            const double a = fmin(1.0, 0.99 * R::min(fmin(bn / bd, als)));
 #pragma unroll
             for (int j = 0; j < N; ++j) x[j] += a * dx[j];
 #pragma unroll
-            for (int i = 0; i < M; ++i) {
-                if (valid(i, o)) {
-                    s[i] += a * ds[i];
-                    z[i] += a * dz[i];
+            for (int k = 0; k < M; ++k) {
+                r[k] += a * u[k];
+                if (vrow(k)) {
+                    s[k] += a * ds[k];
+                    z[k] += a * dz[k];
                 }
             }
         }
@@ -696,18 +733,129 @@ struct Solver {
         return st;
     }
 
-    // -------- FD envelope gradient, proximity_gradient.py:8-88 -------------------------
-    // f_k(theta_k) = sum over rows of primitive k of z_i (G_i(theta_k) x - h_i(theta_k))
-    DCOL_HD double lag_part(const KArgs& A, const DevShape& S, int k, int slot, const double th[6]) const {
+    // Newton direction.  Predictor (cp == nullptr): lambda\ds = lambda\(-lambda o lambda).
+    // Corrector: lambda\ds = lambda\(-lambda o lambda - cp + smu e).  Then
+    // b~z = W^-1(-rz - W lds); dx = (G~'G~)^-1(-rx + G' W^-1 b~z);
+    // dz = W^-1(W^-1 G dx - b~z); ds = W(lds - W dz)          (pdip.py:424-460)
+    DCOL_HD void direction(const SocState* so, const double* il, const double (&F)[N][N], const double (&idg)[N],
+                           const double* rx, const double* cp, double smu, double* dx, double* ds, double* dz,
+                           double* uout) const {
+        double rhs[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) rhs[j] = 0.0;
+        // pass 1: right-hand side
+#pragma unroll
+        for (int k = 0; k < OR; ++k) {
+            const double lds = orth_lds(k, il, cp, smu);
+            const double t = orth_bzt(k, il, lds) * (z[k] * il[k]);    // W^-1 b~z
+#pragma unroll
+            for (int j = 0; j < N; ++j) rhs[j] += G[k][j] * t;
+        }
+        double sbzt[SSA][4], slds[SSA][4];
+#pragma unroll
+        for (int b = 0; b < SS; ++b) {
+            const int k0 = OR + 4 * b;
+            soc_lds(so[b], cp ? cp + k0 : nullptr, smu, slds[b]);
+            double t1[4], t2[4];
+            soc_mul(so[b].W, slds[b], t1);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) t1[e] = -(s[k0 + e] + r[k0 + e]) - t1[e];
+            soc_solve(so[b].W, t1, sbzt[b]);
+            soc_solve(so[b].W, sbzt[b], t2);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int j = 0; j < N; ++j) rhs[j] += G[k0 + e][j] * t2[e];
+        }
+        allsum_vec(rhs);
+#pragma unroll
+        for (int j = 0; j < N; ++j) rhs[j] -= rx[j];
+        chol_solve(F, idg, rhs, dx);
+        // pass 2: dz, ds
+#pragma unroll
+        for (int k = 0; k < OR; ++k) {
+            const double lds = orth_lds(k, il, cp, smu);
+            const double bzt = orth_bzt(k, il, lds);
+            const double wi = z[k] * il[k], w = s[k] * il[k];
+            const double u = rowdot(k, dx);
+            if (uout) uout[k] = u;
+            dz[k] = wi * (wi * u - bzt);
+            ds[k] = w * (lds - w * dz[k]);
+        }
+#pragma unroll
+        for (int b = 0; b < SS; ++b) {
+            const int k0 = OR + 4 * b;
+            double v[4], t[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                v[e] = rowdot(k0 + e, dx);
+                if (uout) uout[k0 + e] = v[e];
+            }
+            soc_solve(so[b].W, v, t);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) t[e] -= sbzt[b][e];
+            soc_solve(so[b].W, t, dz + k0);
+            soc_mul(so[b].W, dz + k0, t);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) t[e] = slds[b][e] - t[e];
+            soc_mul(so[b].W, t, ds + k0);
+        }
+    }
+    // orthant lambda\ds: predictor -(s z)/lambda, corrector (-(s z) - cp + smu)/lambda
+    DCOL_HD double orth_lds(int k, const double* il, const double* cp, double smu) const {
+        const double ll = s[k] * z[k];
+        const double num = cp ? (-ll - cp[k] + smu) : -ll;
+        return num * il[k];
+    }
+    // orthant b~z = w^-1 (-rz - w lds), rz = s + (G x - h)
+    DCOL_HD double orth_bzt(int k, const double* il, double lds) const {
+        const double wi = z[k] * il[k], w = s[k] * il[k];
+        return wi * (-(s[k] + r[k]) - w * lds);
+    }
+    DCOL_HD static void soc_lds(const SocState& S, const double* cp, double smu, double* out) {
+        double v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = -S.ll[e] - (cp ? cp[e] : 0.0);
+        if (cp) v[0] += smu;
+        soc_iprod(S.lam, v, out);
+    }
+    // ratio tests of s + a ds >= 0, z + a dz >= 0 over the lane's rows
+    DCOL_HD void step_bound(const SocState* so, const double* ds, const double* dz, double& bn, double& bd,
+                            double& als) const {
+#pragma unroll
+        for (int k = 0; k < OR; ++k) {
+            if (vort(k)) {
+                ratio(s[k], ds[k], bn, bd);
+                ratio(z[k], dz[k], bn, bd);
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < SS; ++b) {
+            if (vs[b]) {
+                const int k0 = OR + 4 * b;
+                als = fmin(als, fmin(soc_ls(s + k0, ds + k0), soc_ls(z + k0, dz + k0)));
+            }
+        }
+        (void)so;
+    }
+
+    // -------- gradient helpers ---------------------------------------------------------
+    DCOL_HD bool owns_row(int k, int prim) const {
+        const int i = k * LPP + q;
+        return prim == 0 ? (i < o1) : (i >= o1 && i < o);
+    }
+
+    // lane part of f_k(theta_k) = sum over rows of primitive k of z_i (G_i(theta_k) x - h_i(theta_k))
+    DCOL_HD double lag_part(const KArgs& A, const DevShape& S, int prim, const double th[6]) const {
         Frame Fr;
         make_frame(S, th, Fr);
         const double* __restrict__ rows = reinterpret_cast<const double*>(A.rows);
         double acc = 0.0;
 #pragma unroll
-        for (int i = 0; i < OMAX; ++i) {
-            const bool own = (k == 0) ? (i < o1) : (i >= o1 && i < o);
-            if (own) {
-                const int ri = S.row_off + ((k == 0) ? i : (i - o1));
+        for (int k = 0; k < OR; ++k) {
+            if (owns_row(k, prim)) {
+                const int i = k * LPP + q;
+                const int ri = S.row_off + ((prim == 0) ? i : (i - o1));
                 const double2* rw = reinterpret_cast<const double2*>(rows + 8 * (int64_t)ri);
                 const double2 q0 = rw[0], q1 = rw[1], q2 = rw[2];
                 const double u0 = Fr.Qe[0] * q0.x + Fr.Qe[1] * q0.y + Fr.Qe[2] * q1.x;
@@ -717,96 +865,97 @@ struct Solver {
                 if constexpr (N > 4) gx += q2.x * x[4];
                 if constexpr (N > 5) gx += q2.y * x[5];
                 const double hh = u0 * Fr.re[0] + u1 * Fr.re[1] + u2 * Fr.re[2];
-                acc += z[i] * (gx - hh);
+                acc += z[k] * (gx - hh);
             }
         }
 #pragma unroll
-        for (int b = 0; b < NSOC; ++b) {
-            if (b == slot) {
+        for (int b = 0; b < SS; ++b) {
+            if (vs[b] && soc_owner[b] == prim) {
                 double Gb[4][N], hb[4];
                 soc_rows(S.soc_kind, S.R, S.cone_c, S.tanb, S.n_extra, Fr.Qe, Fr.re, Gb, hb);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    double gx = Gb[r][0] * x[0];
+                for (int e = 0; e < 4; ++e) {
+                    double gx = Gb[e][0] * x[0];
 #pragma unroll
-                    for (int j = 1; j < N; ++j) gx += Gb[r][j] * x[j];
-                    acc += z[OMAX + 4 * b + r] * (gx - hb[r]);
+                    for (int j = 1; j < N; ++j) gx += Gb[e][j] * x[j];
+                    acc += z[OR + 4 * b + e] * (gx - hb[e]);
                 }
             }
         }
         return acc;
     }
 
-    // scipy approx_fprime(theta, f, sqrt(eps)) restricted to primitive k's 6 coordinates
-    DCOL_HD void fd_grad_prim(const KArgs& A, const DevShape& S, int k, int slot,
-                                                 const double th0[6], double* g) const {
+    // scipy approx_fprime(theta, f, sqrt(eps)) restricted to primitive prim's 6 coordinates
+    DCOL_HD void fd_grad_prim(const KArgs& A, const DevShape& S, int prim, const double th0[6], double* g) const {
         const double hstep = 1.4901161193847656e-08;   // sqrt(finfo(float).eps)
-        const double f0 = lag_part(A, S, k, slot, th0);
+        const double f0 = R::sum(lag_part(A, S, prim, th0));
 #pragma unroll 1
         for (int j = 0; j < 6; ++j) {
             double th[6];
 #pragma unroll
-            for (int q = 0; q < 6; ++q) th[q] = th0[q];
+            for (int c = 0; c < 6; ++c) th[c] = th0[c];
             double hj = hstep;
             if ((th0[j] + hstep) - th0[j] == 0.0)       // _numdiff: fall back to a relative step
                 hj = hstep * (th0[j] >= 0.0 ? 1.0 : -1.0) * fmax(1.0, fabs(th0[j]));
             th[j] = th0[j] + hj;
             const double dxj = th[j] - th0[j];
-            g[j] = (lag_part(A, S, k, slot, th) - f0) / dxj;
+            g[j] = (R::sum(lag_part(A, S, prim, th)) - f0) / dxj;
         }
     }
 
-    // d/dtheta_k of z'(G(theta)x - h(theta)) in closed form.  Every row of primitive k reads
-    // value_i = u_i.(x[0:3] - r_eff) + (theta-free terms) + ex_i(Qe).x[4:], with u_i = Qe a_i
-    // (rotated rows: polytope/cone/cylinder orthant rows, cone SOC rows) or u = -e_k
-    // (ball SOC rows).  With w = sum z_i a_i (rotated rows, body frame), zeta = z of the ball
-    // SOC rows 1..3, xi = (x4, x5, 0) restricted to the extra columns:
-    //   d/dr   = zeta - Qe w
-    //   d/dp_j = d' Q_j (Qoff w) - (Qe w - zeta)' Q_j r_off + zeta' Q_j (Qoff xi)
-    DCOL_HD void env_grad_prim(const KArgs& A, const DevShape& S, int k, int slot,
-                                                  const double th[6], double* g) const {
+    // closed-form d/dtheta_k of z'(G(theta)x - h(theta)) (see DESIGN.md "gradient modes"):
+    //   d/dr = zeta - Qe w;  d/dp_j = d' Q_j (Qoff w) - (Qe w - zeta)' Q_j r_off + zeta' Q_j (Qoff xi)
+    // w = sum z_i a_i over rotated rows (body frame), zeta = z of the ball SOC rows 1..3,
+    // xi = (x4, x5, 0) on the extra columns, d = x[0:3] - r_eff
+    DCOL_HD void env_grad_prim(const KArgs& A, const DevShape& S, int prim, const double th[6], double* g) const {
         Frame Fr;
         make_frame(S, th, Fr);
         const double* __restrict__ rows = reinterpret_cast<const double*>(A.rows);
-        double w[3] = {0.0, 0.0, 0.0};
+        double w[3] = {0.0, 0.0, 0.0}, zeta[3] = {0.0, 0.0, 0.0};
 #pragma unroll
-        for (int i = 0; i < OMAX; ++i) {
-            const bool own = (k == 0) ? (i < o1) : (i >= o1 && i < o);
-            if (own) {
-                const int ri = S.row_off + ((k == 0) ? i : (i - o1));
+        for (int k = 0; k < OR; ++k) {
+            if (owns_row(k, prim)) {
+                const int i = k * LPP + q;
+                const int ri = S.row_off + ((prim == 0) ? i : (i - o1));
                 const double2* rw = reinterpret_cast<const double2*>(rows + 8 * (int64_t)ri);
                 const double2 q0 = rw[0], q1 = rw[1];
-                w[0] += z[i] * q0.x;
-                w[1] += z[i] * q0.y;
-                w[2] += z[i] * q1.x;
+                w[0] += z[k] * q0.x;
+                w[1] += z[k] * q0.y;
+                w[2] += z[k] * q1.x;
             }
         }
-        double zeta[3] = {0.0, 0.0, 0.0};
-        double xi[3] = {0.0, 0.0, 0.0};
 #pragma unroll
-        for (int b = 0; b < NSOC; ++b) {
-            if (b == slot) {
-                const double* zb = z + OMAX + 4 * b;
+        for (int b = 0; b < SS; ++b) {
+            if (vs[b] && soc_owner[b] == prim) {
+                const double* zb = z + OR + 4 * b;
                 if (S.soc_kind == SOC_CONE) {
                     w[0] -= zb[0] * S.tanb;     // a_k = -E_kk e_k
                     w[1] -= zb[1];
                     w[2] -= zb[2];
                 } else {
                     zeta[0] = zb[1]; zeta[1] = zb[2]; zeta[2] = zb[3];
-                    if constexpr (N > 4) xi[0] = (S.n_extra >= 1) ? x[4] : 0.0;
-                    if constexpr (N > 5) xi[1] = (S.n_extra >= 2) ? x[5] : 0.0;
                 }
             }
         }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            w[c] = R::sum(w[c]);
+            zeta[c] = R::sum(zeta[c]);
+        }
+        double xi[3] = {0.0, 0.0, 0.0};
+        if (S.soc_kind == SOC_BALL) {
+            if constexpr (N > 4) xi[0] = (S.n_extra >= 1) ? x[4] : 0.0;
+            if constexpr (N > 5) xi[1] = (S.n_extra >= 2) ? x[5] : 0.0;
+        }
         double e[3], d[3], c1[3], c2[3];
 #pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            const double qw = Fr.Qe[3 * r] * w[0] + Fr.Qe[3 * r + 1] * w[1] + Fr.Qe[3 * r + 2] * w[2];
-            e[r] = qw - zeta[r];
-            g[r] = -e[r];
-            d[r] = x[r] - Fr.re[r];
-            c1[r] = S.Q_off[3 * r] * w[0] + S.Q_off[3 * r + 1] * w[1] + S.Q_off[3 * r + 2] * w[2];
-            c2[r] = S.Q_off[3 * r] * xi[0] + S.Q_off[3 * r + 1] * xi[1] + S.Q_off[3 * r + 2] * xi[2];
+        for (int rr = 0; rr < 3; ++rr) {
+            const double qw = Fr.Qe[3 * rr] * w[0] + Fr.Qe[3 * rr + 1] * w[1] + Fr.Qe[3 * rr + 2] * w[2];
+            e[rr] = qw - zeta[rr];
+            g[rr] = -e[rr];
+            d[rr] = x[rr] - Fr.re[rr];
+            c1[rr] = S.Q_off[3 * rr] * w[0] + S.Q_off[3 * rr + 1] * w[1] + S.Q_off[3 * rr + 2] * w[2];
+            c2[rr] = S.Q_off[3 * rr] * xi[0] + S.Q_off[3 * rr + 1] * xi[1] + S.Q_off[3 * rr + 2] * xi[2];
         }
         double dQ[3][9];
         dcm_jacobian(th + 3, dQ);
@@ -814,12 +963,12 @@ struct Solver {
         for (int j = 0; j < 3; ++j) {
             double acc = 0.0;
 #pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                const double* q = &dQ[j][3 * r];
-                const double m1 = q[0] * c1[0] + q[1] * c1[1] + q[2] * c1[2];
-                const double m2 = q[0] * S.r_off[0] + q[1] * S.r_off[1] + q[2] * S.r_off[2];
-                const double m3 = q[0] * c2[0] + q[1] * c2[1] + q[2] * c2[2];
-                acc += d[r] * m1 - e[r] * m2 + zeta[r] * m3;
+            for (int rr = 0; rr < 3; ++rr) {
+                const double* qq = &dQ[j][3 * rr];
+                const double m1 = qq[0] * c1[0] + qq[1] * c1[1] + qq[2] * c1[2];
+                const double m2 = qq[0] * S.r_off[0] + qq[1] * S.r_off[1] + qq[2] * S.r_off[2];
+                const double m3 = qq[0] * c2[0] + qq[1] * c2[1] + qq[2] * c2[2];
+                acc += d[rr] * m1 - e[rr] * m2 + zeta[rr] * m3;
             }
             g[3 + j] = acc;
         }
@@ -829,25 +978,25 @@ struct Solver {
 // ------------------------------------------------------------------------------------
 // kernel
 // ------------------------------------------------------------------------------------
-template <int N, int NSOC, int OMAX>
-DCOL_HD void solve_one(const KArgs& A, int64_t pi) {
+template <int N, int NSOC, int OMAX, int LPP>
+DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
     const int64_t B = A.B;
     const int k1 = A.s1[pi], k2 = A.s2[pi];
     const DevShape& S1 = A.shapes[k1];
     const DevShape& S2 = A.shapes[k2];
     double th1[6], th2[6];
 #pragma unroll
-    for (int q = 0; q < 6; ++q) {
-        th1[q] = A.pose1[q * B + pi];
-        th2[q] = A.pose2[q * B + pi];
+    for (int c = 0; c < 6; ++c) {
+        th1[c] = A.pose1[c * B + pi];
+        th2[c] = A.pose2[c * B + pi];
     }
     Frame F1, F2;
     make_frame(S1, th1, F1);
     make_frame(S2, th2, F2);
 
-    Solver<N, NSOC, OMAX> P;
-    int slot_owner[2];
-    P.assemble(A, S1, S2, F1, F2, slot_owner);
+    Solver<N, NSOC, OMAX, LPP> P;
+    P.q = q;
+    P.assemble(A, S1, S2, F1, F2);
     int it = 0;
     int32_t st;
     if (!P.initialize()) st = ST_NOT_PD;
@@ -855,41 +1004,55 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi) {
 
     const double nan = __builtin_nan("");
     const bool ok = st == ST_OK;
+    double g[12];
+    const bool want_grad = (A.flags & (F_GRAD_FD | F_GRAD_ENV)) && A.grad;
+    if (want_grad) {
+        // Phase boundary: make the gradient re-read poses, shape records and row descriptors
+        // instead of keeping the assembly-phase copies live across the whole PDIP loop
+        // (register pressure: ~150 -> ~300 VGPRs without this).
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            th1[c] = A.pose1[c * B + pi];
+            th2[c] = A.pose2[c * B + pi];
+        }
+        if (ok) {
+            if (A.flags & F_GRAD_ENV) {
+                P.env_grad_prim(A, S1, 0, th1, g);
+                P.env_grad_prim(A, S2, 1, th2, g + 6);
+            } else {
+                P.fd_grad_prim(A, S1, 0, th1, g);
+                P.fd_grad_prim(A, S2, 1, th2, g + 6);
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 12; ++c) g[c] = nan;
+        }
+    }
+    if (q != 0) return;
     A.alpha[pi] = ok ? P.x[3] : nan;
     if (A.iters) A.iters[pi] = it;
     if (A.status) A.status[pi] = st;
     if ((A.flags & F_CONTACT) && A.contact) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) A.contact[q * B + pi] = ok ? P.x[q] : nan;
+        for (int c = 0; c < 3; ++c) A.contact[c * B + pi] = ok ? P.x[c] : nan;
     }
-    if ((A.flags & (F_GRAD_FD | F_GRAD_ENV)) && A.grad) {
-        double g[12];
-        if (ok) {
-            const int slot1 = (S1.soc_kind != SOC_NONE) ? 0 : -1;
-            const int slot2 = (S2.soc_kind != SOC_NONE) ? ((S1.soc_kind != SOC_NONE) ? 1 : 0) : -1;
-            if (A.flags & F_GRAD_ENV) {
-                P.env_grad_prim(A, S1, 0, slot1, th1, g);
-                P.env_grad_prim(A, S2, 1, slot2, th2, g + 6);
-            } else {
-                P.fd_grad_prim(A, S1, 0, slot1, th1, g);
-                P.fd_grad_prim(A, S2, 1, slot2, th2, g + 6);
-            }
-        } else {
+    if (want_grad) {
 #pragma unroll
-            for (int q = 0; q < 12; ++q) g[q] = nan;
-        }
-#pragma unroll
-        for (int q = 0; q < 12; ++q) A.grad[q * B + pi] = g[q];
+        for (int c = 0; c < 12; ++c) A.grad[c * B + pi] = g[c];
     }
 }
 
-// One lane per pair.  Slots [slot0, slot0+n) of the plan's permutation (or identity).
-template <int N, int NSOC, int OMAX>
+// LPP lanes per pair; slots [slot0, slot0+n) of the plan's permutation (or identity).
+// The n*LPP threads of a launch are contiguous, so a group never straddles the tail.
+template <int N, int NSOC, int OMAX, int LPP>
 __global__ void __launch_bounds__(256) prox_kernel(KArgs A) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= A.n) return;
-    const int64_t pi = A.perm ? (int64_t)A.perm[A.slot0 + t] : (A.slot0 + t);
-    solve_one<N, NSOC, OMAX>(A, pi);
+    const int64_t slot = t / LPP;
+    const int q = (int)(t % LPP);
+    if (slot >= A.n) return;
+    const int64_t pi = A.perm ? (int64_t)A.perm[A.slot0 + slot] : (A.slot0 + slot);
+    solve_one<N, NSOC, OMAX, LPP>(A, pi, q);
 }
 
 }  // namespace dcol

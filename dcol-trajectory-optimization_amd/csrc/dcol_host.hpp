@@ -2,6 +2,7 @@
 // C-ABI (dcol_capi.cpp) and the test-only x86 emulator (tests/emul).
 #pragma once
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -30,12 +31,30 @@ inline const std::map<std::pair<int, int>, std::vector<int>>& buckets() {
     static const std::map<std::pair<int, int>, std::vector<int>> m = [] {
         std::map<std::pair<int, int>, std::vector<int>> r;
 #define DCOL_ADD(NN, NS, OM) r[{NN, NS}].push_back(OM);
-        DCOL_VARIANTS(DCOL_ADD)
+        DCOL_SHAPES(DCOL_ADD)
 #undef DCOL_ADD
         for (auto& kv : r) std::sort(kv.second.begin(), kv.second.end());
         return r;
     }();
     return m;
+}
+
+// lanes per pair for a kernel shape: the first compiled LPP, or DCOL_LPP=<n> if that
+// alternative is compiled for the shape (A/B experiments)
+inline int choose_lpp(int N, int nsoc, int omax) {
+    static const int forced = [] {
+        const char* e = std::getenv("DCOL_LPP");
+        return e ? std::atoi(e) : 0;
+    }();
+    int first = 0;
+#define DCOL_PICK(NN, NS, OM, LP)                                  \
+    if (NN == N && NS == nsoc && OM == omax) {                     \
+        if (first == 0) first = LP;                                \
+        if (forced == LP) return LP;                               \
+    }
+    DCOL_VARIANTS(DCOL_PICK)
+#undef DCOL_PICK
+    return first;
 }
 
 // Static digest of one primitive (misc_primitive_constructor.py:4-88 ->
@@ -108,11 +127,11 @@ inline int digest_shape(const dcol_shape_desc& d, int32_t idx, DevShape& S, std:
 
 struct PairClass {
     int32_t status;   // OK / UNSUPPORTED / TOO_LARGE
-    int N, nsoc, o, omax;
+    int N, nsoc, o, omax, lpp;
 };
 
 inline PairClass classify(const DevShape& a, const DevShape& b) {
-    PairClass c{DCOL_OK, 4, 0, 0, 0};
+    PairClass c{DCOL_OK, 4, 0, 0, 0, 0};
     if (a.n_extra > 0 && b.n_extra > 0) {   // combine_problem_matrices.py:58-67 (case 4)
         c.status = DCOL_UNSUPPORTED;
         return c;
@@ -128,6 +147,7 @@ inline PairClass classify(const DevShape& a, const DevShape& b) {
     for (int om : it->second)
         if (om >= std::max(c.o, 1)) {
             c.omax = om;
+            c.lpp = choose_lpp(c.N, c.nsoc, om);
             return c;
         }
     c.status = DCOL_TOO_LARGE;

@@ -5,7 +5,7 @@
 
 namespace dcol {
 constexpr int kBlock = 256;   // 4 waves; one lane per pair
-hipError_t launch_n4(int nsoc, int omax, const KArgs& args, int64_t grid, hipStream_t stream);
-hipError_t launch_n5(int nsoc, int omax, const KArgs& args, int64_t grid, hipStream_t stream);
-hipError_t launch_n6(int nsoc, int omax, const KArgs& args, int64_t grid, hipStream_t stream);
+hipError_t launch_n4(int nsoc, int omax, int lpp, const KArgs& args, hipStream_t stream);
+hipError_t launch_n5(int nsoc, int omax, int lpp, const KArgs& args, hipStream_t stream);
+hipError_t launch_n6(int nsoc, int omax, int lpp, const KArgs& args, hipStream_t stream);
 }  // namespace dcol

@@ -56,8 +56,8 @@ extern "C" int dcol_emul_batch(const dcol_shape_desc* shapes, int32_t n, int64_t
             continue;
         }
 #define DCOL_EMUL(NN, NS, OM) \
-        if (c.N == NN && c.nsoc == NS && c.omax == OM) { solve_one<NN, NS, OM>(A, i); continue; }
-        DCOL_VARIANTS(DCOL_EMUL)
+        if (c.N == NN && c.nsoc == NS && c.omax == OM) { solve_one<NN, NS, OM, 1>(A, i, 0); continue; }
+        DCOL_SHAPES(DCOL_EMUL)
 #undef DCOL_EMUL
         return fail(DCOL_ERR_ARG, "no variant");
     }
