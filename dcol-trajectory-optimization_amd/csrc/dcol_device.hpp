@@ -274,9 +274,11 @@ __device__ __forceinline__ double dpp_d(double v) {
 }
 #define DCOL_XOR1(v) dpp_d<0xB1>(v)   // quad_perm [1,0,3,2]
 #define DCOL_XOR2(v) dpp_d<0x4E>(v)   // quad_perm [2,3,0,1]
+#define DCOL_HMIR(v) dpp_d<0x141>(v)  // row_half_mirror: lane i <-> 7-i within 8 lanes
 #else
 #define DCOL_XOR1(v) (__builtin_trap(), (v))   // multi-lane groups run on the GPU only
 #define DCOL_XOR2(v) (__builtin_trap(), (v))
+#define DCOL_HMIR(v) (__builtin_trap(), (v))
 #endif
 
 template <int LPP>
@@ -292,6 +294,26 @@ struct Grp<2> {
     DCOL_HD static double sum(double v) { return v + DCOL_XOR1(v); }
     DCOL_HD static double min(double v) { return fmin(v, DCOL_XOR1(v)); }
     DCOL_HD static double max(double v) { return fmax(v, DCOL_XOR1(v)); }
+};
+template <>
+struct Grp<8> {
+    // after the two quad steps every lane holds its quad's value; the half-row mirror pairs
+    // each lane with one of the other quad
+    DCOL_HD static double sum(double v) {
+        v = v + DCOL_XOR1(v);
+        v = v + DCOL_XOR2(v);
+        return v + DCOL_HMIR(v);
+    }
+    DCOL_HD static double min(double v) {
+        v = fmin(v, DCOL_XOR1(v));
+        v = fmin(v, DCOL_XOR2(v));
+        return fmin(v, DCOL_HMIR(v));
+    }
+    DCOL_HD static double max(double v) {
+        v = fmax(v, DCOL_XOR1(v));
+        v = fmax(v, DCOL_XOR2(v));
+        return fmax(v, DCOL_HMIR(v));
+    }
 };
 template <>
 struct Grp<4> {
@@ -688,7 +710,7 @@ struct Solver {
             // ---- predictor (affine) direction
             double dsA[M], dzA[M];
             double dx[N];
-            direction(so, il, F, idg, rx, nullptr, 0.0, dx, dsA, dzA, nullptr);
+            direction(so, il, F, idg, rx, nullptr, 0.0, dx, dsA, dzA);
             double bn = 1.0, bd = 1.0, als = 1.0;
             step_bound(so, dsA, dzA, bn, bd, als);
             const double aa = R::min(fmin(bn / bd, als));           // quirk Q5 (no 0.99)
@@ -712,20 +734,53 @@ struct Solver {
                 soc_prod(t1, t2, cp + k0);
             }
 
-            // ---- corrector (combined) direction
-            double ds[M], dz[M], u[M];
-            direction(so, il, F, idg, rx, cp, sigma * mu, dx, ds, dz, u);
+            // ---- corrector (combined) direction.  ds/dz/G dx are consumed by the ratio
+            // test as they are produced and recomputed in the update (register budget).
+            const double smu = sigma * mu;
+            double sbzt[SSA][4], slds[SSA][4];
+            rhs_solve(so, il, F, idg, rx, cp, smu, dx, sbzt, slds);
             bn = 1.0; bd = 1.0; als = 1.0;
-            step_bound(so, ds, dz, bn, bd, als);
+#pragma unroll
+            for (int k = 0; k < OR; ++k) {
+                double u, dzk, dsk;
+                orth_step(k, il, cp, smu, dx, u, dzk, dsk);
+                if (vort(k)) {
+                    ratio(s[k], dsk, bn, bd);
+                    ratio(z[k], dzk, bn, bd);
+                }
+            }
+            double sdz[SSA][4], sds[SSA][4], su[SSA][4];
+#pragma unroll
+            for (int b = 0; b < SS; ++b) {
+                soc_step(so[b], OR + 4 * b, sbzt[b], slds[b], dx, su[b], sdz[b], sds[b]);
+                if (vs[b]) {
+                    const int k0 = OR + 4 * b;
+                    als = fmin(als, fmin(soc_ls(s + k0, sds[b]), soc_ls(z + k0, sdz[b])));
+                }
+            }
             const double a = fmin(1.0, 0.99 * R::min(fmin(bn / bd, als)));
 #pragma unroll
             for (int j = 0; j < N; ++j) x[j] += a * dx[j];
 #pragma unroll
-            for (int k = 0; k < M; ++k) {
-                r[k] += a * u[k];
-                if (vrow(k)) {
-                    s[k] += a * ds[k];
-                    z[k] += a * dz[k];
+            for (int k = 0; k < OR; ++k) {
+                double u, dzk, dsk;
+                orth_step(k, il, cp, smu, dx, u, dzk, dsk);
+                r[k] += a * u;
+                if (vort(k)) {
+                    s[k] += a * dsk;
+                    z[k] += a * dzk;
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < SS; ++b) {
+                const int k0 = OR + 4 * b;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    r[k0 + e] += a * su[b][e];
+                    if (vs[b]) {
+                        s[k0 + e] += a * sds[b][e];
+                        z[k0 + e] += a * sdz[b][e];
+                    }
                 }
             }
         }
@@ -737,13 +792,12 @@ struct Solver {
     // Corrector: lambda\ds = lambda\(-lambda o lambda - cp + smu e).  Then
     // b~z = W^-1(-rz - W lds); dx = (G~'G~)^-1(-rx + G' W^-1 b~z);
     // dz = W^-1(W^-1 G dx - b~z); ds = W(lds - W dz)          (pdip.py:424-460)
-    DCOL_HD void direction(const SocState* so, const double* il, const double (&F)[N][N], const double (&idg)[N],
-                           const double* rx, const double* cp, double smu, double* dx, double* ds, double* dz,
-                           double* uout) const {
+    DCOL_HD void rhs_solve(const SocState* so, const double* il, const double (&F)[N][N], const double (&idg)[N],
+                           const double* rx, const double* cp, double smu, double* dx, double (*sbzt)[4],
+                           double (*slds)[4]) const {
         double rhs[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) rhs[j] = 0.0;
-        // pass 1: right-hand side
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
             const double lds = orth_lds(k, il, cp, smu);
@@ -751,7 +805,6 @@ struct Solver {
 #pragma unroll
             for (int j = 0; j < N; ++j) rhs[j] += G[k][j] * t;
         }
-        double sbzt[SSA][4], slds[SSA][4];
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
             const int k0 = OR + 4 * b;
@@ -771,34 +824,45 @@ struct Solver {
 #pragma unroll
         for (int j = 0; j < N; ++j) rhs[j] -= rx[j];
         chol_solve(F, idg, rhs, dx);
-        // pass 2: dz, ds
+    }
+    // one orthant row of the step: u = G_k dx, dz = w^-1(w^-1 u - b~z), ds = w(lds - w dz)
+    DCOL_HD void orth_step(int k, const double* il, const double* cp, double smu, const double* dx, double& u,
+                           double& dz, double& ds) const {
+        const double lds = orth_lds(k, il, cp, smu);
+        const double bzt = orth_bzt(k, il, lds);
+        const double wi = z[k] * il[k], w = s[k] * il[k];
+        u = rowdot(k, dx);
+        dz = wi * (wi * u - bzt);
+        ds = w * (lds - w * dz);
+    }
+    DCOL_HD void soc_step(const SocState& S, int k0, const double* bzt, const double* lds, const double* dx, double* u,
+                          double* dz, double* ds) const {
+        double t[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) u[e] = rowdot(k0 + e, dx);
+        soc_solve(S.W, u, t);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t[e] -= bzt[e];
+        soc_solve(S.W, t, dz);
+        soc_mul(S.W, dz, t);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t[e] = lds[e] - t[e];
+        soc_mul(S.W, t, ds);
+    }
+    // full direction with stored ds/dz (predictor: they feed rho and the corrector's cp)
+    DCOL_HD void direction(const SocState* so, const double* il, const double (&F)[N][N], const double (&idg)[N],
+                           const double* rx, const double* cp, double smu, double* dx, double* ds, double* dz) const {
+        double sbzt[SSA][4], slds[SSA][4];
+        rhs_solve(so, il, F, idg, rx, cp, smu, dx, sbzt, slds);
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
-            const double lds = orth_lds(k, il, cp, smu);
-            const double bzt = orth_bzt(k, il, lds);
-            const double wi = z[k] * il[k], w = s[k] * il[k];
-            const double u = rowdot(k, dx);
-            if (uout) uout[k] = u;
-            dz[k] = wi * (wi * u - bzt);
-            ds[k] = w * (lds - w * dz[k]);
+            double u;
+            orth_step(k, il, cp, smu, dx, u, dz[k], ds[k]);
         }
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
-            const int k0 = OR + 4 * b;
-            double v[4], t[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                v[e] = rowdot(k0 + e, dx);
-                if (uout) uout[k0 + e] = v[e];
-            }
-            soc_solve(so[b].W, v, t);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) t[e] -= sbzt[b][e];
-            soc_solve(so[b].W, t, dz + k0);
-            soc_mul(so[b].W, dz + k0, t);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) t[e] = slds[b][e] - t[e];
-            soc_mul(so[b].W, t, ds + k0);
+            double u[4];
+            soc_step(so[b], OR + 4 * b, sbzt[b], slds[b], dx, u, dz + OR + 4 * b, ds + OR + 4 * b);
         }
     }
     // orthant lambda\ds: predictor -(s z)/lambda, corrector (-(s z) - cp + smu)/lambda
@@ -978,6 +1042,16 @@ struct Solver {
 // ------------------------------------------------------------------------------------
 // kernel
 // ------------------------------------------------------------------------------------
+// Hide a pointer's provenance from the optimiser (forces fresh loads through it).
+template <typename P>
+DCOL_HD void launder(P& p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+s"(p));
+#else
+    asm volatile("" : "+r"(p));
+#endif
+}
+
 template <int N, int NSOC, int OMAX, int LPP>
 DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
     const int64_t B = A.B;
@@ -1011,18 +1085,25 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
         // instead of keeping the assembly-phase copies live across the whole PDIP loop
         // (register pressure: ~150 -> ~300 VGPRs without this).
         asm volatile("" ::: "memory");
+        KArgs L = A;   // laundered copies of the table pointers: no load CSE across the loop
+        launder(L.shapes);
+        launder(L.rows);
+        launder(L.pose1);
+        launder(L.pose2);
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
-            th1[c] = A.pose1[c * B + pi];
-            th2[c] = A.pose2[c * B + pi];
+            th1[c] = L.pose1[c * B + pi];
+            th2[c] = L.pose2[c * B + pi];
         }
+        const DevShape& T1 = L.shapes[k1];
+        const DevShape& T2 = L.shapes[k2];
         if (ok) {
             if (A.flags & F_GRAD_ENV) {
-                P.env_grad_prim(A, S1, 0, th1, g);
-                P.env_grad_prim(A, S2, 1, th2, g + 6);
+                P.env_grad_prim(L, T1, 0, th1, g);
+                P.env_grad_prim(L, T2, 1, th2, g + 6);
             } else {
-                P.fd_grad_prim(A, S1, 0, th1, g);
-                P.fd_grad_prim(A, S2, 1, th2, g + 6);
+                P.fd_grad_prim(L, T1, 0, th1, g);
+                P.fd_grad_prim(L, T2, 1, th2, g + 6);
             }
         } else {
 #pragma unroll
@@ -1045,8 +1126,9 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
 
 // LPP lanes per pair; slots [slot0, slot0+n) of the plan's permutation (or identity).
 // The n*LPP threads of a launch are contiguous, so a group never straddles the tail.
-template <int N, int NSOC, int OMAX, int LPP>
-__global__ void __launch_bounds__(256) prox_kernel(KArgs A) {
+// WPS = minimum waves per SIMD requested from the register allocator (variants.py).
+template <int N, int NSOC, int OMAX, int LPP, int WPS>
+__global__ void __launch_bounds__(256, WPS) prox_kernel(KArgs A) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t slot = t / LPP;
     const int q = (int)(t % LPP);

@@ -47,7 +47,7 @@ inline int choose_lpp(int N, int nsoc, int omax) {
         return e ? std::atoi(e) : 0;
     }();
     int first = 0;
-#define DCOL_PICK(NN, NS, OM, LP)                                  \
+#define DCOL_PICK(NN, NS, OM, LP, WP)                              \
     if (NN == N && NS == nsoc && OM == omax) {                     \
         if (first == 0) first = LP;                                \
         if (forced == LP) return LP;                               \

@@ -1,0 +1,87 @@
+"""Multi-rank sharding + all-gather (dcol_amd.dist) on CPU: world_size 2, gloo backend.
+
+Each rank solves its shard with the NumPy oracle (test infrastructure standing in for the
+per-rank GPU engine); the gathered full batch must equal a single-process solve of the
+whole batch exactly (no cross-pair arithmetic exists)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import golden_files, load_golden
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_fn(d, want_grad=True):
+    from oracle import dcol_oracle as O
+
+    def fn(idx):
+        out = O.run_batch(d, d["s1"][idx], d["s2"][idx], d["pose1"][idx], d["pose2"][idx], 1e-6, want_grad)
+        return {"alpha": out["alpha"], "grad": out["grad"], "status": out["status"], "iters": out["iters"]}
+    return fn
+
+
+def _worker(rank, world, port, path, balanced, q):
+    import sys
+    import torch.distributed as dist
+    from conftest import PKG, REPO
+    for p in (PKG, REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from dcol_amd.dist import ShardedBatch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    d = load_golden(path)
+    B = 120
+    d = {k: (v[:B] if k in ("s1", "s2", "pose1", "pose2") else v) for k, v in d.items()}
+    cost = (d["nh"][d["s1"]] + d["nh"][d["s2"]]) if balanced else None
+    sb = ShardedBatch(B, rank, world, cost_key=cost)
+    local = sb.solve(_oracle_fn(d))
+    full = sb.gather(local)
+    if rank == 0:
+        q.put({k: v for k, v in full.items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("balanced", [False, True])
+def test_gloo_world2_gather_equals_single(balanced):
+    path = [p for p in golden_files() if p.endswith("synthetic_mixed.npz")][0]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, path, balanced, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    full = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    d = load_golden(path)
+    ref = _oracle_fn({k: (v[:120] if k in ("s1", "s2", "pose1", "pose2") else v) for k, v in d.items()})(np.arange(120))
+    np.testing.assert_array_equal(full["status"], ref["status"])
+    np.testing.assert_array_equal(full["iters"], ref["iters"])
+    np.testing.assert_array_equal(full["alpha"], ref["alpha"])
+    np.testing.assert_array_equal(full["grad"], ref["grad"])
+
+
+def test_shard_indices_partition():
+    from dcol_amd.dist import shard_indices
+    rng = np.random.default_rng(0)
+    for B in (0, 1, 7, 100, 1001):
+        for world in (1, 2, 3, 8):
+            for cost in (None, rng.integers(0, 5, B)):
+                parts = [shard_indices(B, r, world, cost) for r in range(world)]
+                allidx = np.sort(np.concatenate(parts)) if parts else np.zeros(0)
+                np.testing.assert_array_equal(allidx, np.arange(B))
+                sizes = [len(p) for p in parts]
+                assert max(sizes) - min(sizes) <= 1
