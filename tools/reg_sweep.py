@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Register/occupancy sweep of the solver kernel over (shape, LPP, min waves per SIMD).
+
+For every kernel shape in csrc/variants.py, compiles prox-kernel instantiations with
+LPP in {2, 4, 8} and __launch_bounds__(256, {1, 2}) and prints VGPR/AGPR/scratch/occupancy
+(hipcc -Rpass-analysis=kernel-resource-usage).  Used to pick variants.CONFIG.
+Usage: python3 tools/reg_sweep.py [-j 8]
+"""
+import argparse
+import os
+import re
+import subprocess
+import sys
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
+
+CSRC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "dcol-trajectory-optimization_amd", "csrc")
+sys.path.insert(0, CSRC)
+import variants  # noqa: E402
+
+SRC = """#include "dcol_device.hpp"
+namespace dcol {{
+template <int N, int NS, int OM, int LP>
+__global__ void __launch_bounds__(256, {w}) kb(KArgs A) {{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t slot = t / LP; const int q = (int)(t % LP);
+    if (slot >= A.n) return;
+    solve_one<N, NS, OM, LP>(A, slot, q);
+}}
+template __global__ void kb<{n},{s},{o},{l}>(KArgs); }}
+"""
+
+
+def run(job, tmp):
+    n, s, o, lpp, w = job
+    fn = os.path.join(tmp, f"k_{n}_{s}_{o}_{lpp}_{w}.hip")
+    open(fn, "w").write(SRC.format(n=n, s=s, o=o, l=lpp, w=w))
+    err = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{CSRC}", "-c", fn, "-o", os.devnull,
+                          "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True).stderr
+    last = lambda pat: (re.findall(pat, err) or ["?"])[-1]  # noqa: E731
+    return job, last(r"VGPRs: (\d+)"), last(r"AGPRs: (\d+)"), last(r"ScratchSize \[bytes/lane\]: (\d+)"), \
+        last(r"Occupancy \[waves/SIMD\]: (\d+)")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-j", type=int, default=8)
+    args = ap.parse_args()
+    shapes = [(n, s, o) for (n, s), os_ in sorted(variants.OMAX.items()) for o in os_]
+    jobs = [(n, s, o, l, w) for n, s, o in shapes for l in (2, 4, 8) if o % l == 0 for w in (1, 2)]
+    with tempfile.TemporaryDirectory() as tmp, ThreadPoolExecutor(args.j) as ex:
+        for job, v, a, sc, oc in ex.map(lambda j: run(j, tmp), jobs):
+            print(*job, "vgpr", v, "agpr", a, "scratch", sc, "occ", oc, flush=True)
+
+
+if __name__ == "__main__":
+    main()
