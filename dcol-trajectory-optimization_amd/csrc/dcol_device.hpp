@@ -41,6 +41,35 @@
 
 namespace dcol {
 
+// Fast reciprocal / reciprocal square root: the hardware estimate (v_rcp_f64 / v_rsq_f64)
+// refined by two Newton steps to full double precision (~1 ulp, not correctly rounded --
+// a rounding-level change; the host build used by tests/emul keeps IEEE division).
+DCOL_HD double frcp(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double y = __builtin_amdgcn_rcp(x);
+    double e = __builtin_fma(-x, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    e = __builtin_fma(-x, y, 1.0);
+    return __builtin_fma(y, e, y);
+#else
+    return 1.0 / x;
+#endif
+}
+DCOL_HD double frsqrt(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = 0.5 * y;               // g ~ sqrt(x), h ~ 1/(2 sqrt(x))
+    double r = __builtin_fma(-g, h, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    r = __builtin_fma(-g, h, 0.5);
+    h = __builtin_fma(h, r, h);
+    return h + h;
+#else
+    return 1.0 / sqrt(x);
+#endif
+}
+
 enum : int32_t { ST_OK = 0, ST_MAXITER = 1, ST_UNSUPPORTED = 2, ST_NOT_PD = 3, ST_NONFINITE = 4, ST_TOO_LARGE = 5 };
 enum : int32_t { SOC_NONE = 0, SOC_BALL = 1, SOC_CONE = 2 };
 enum : int32_t { F_GRAD_FD = 1, F_GRAD_ENV = 2, F_CONTACT = 4 };
@@ -100,6 +129,7 @@ struct KArgs {
 struct Frame {
     double Qe[9];  // Q(p) * Q_offset
     double re[3];  // r + Q(p) * r_offset
+    double qro[3]; // Q(p) * r_offset
 };
 
 // dcm_from_mrp, problem_matrices.py:213-251 (same expanded expression)
@@ -107,7 +137,7 @@ DCOL_HD void dcm_from_mrp(double p1, double p2, double p3, double Q[9]) {
     const double s = p1 * p1 + p2 * p2 + p3 * p3 + 1.0;
     const double den = s * s;
     const double a = 4.0 * (p1 * p1) + 4.0 * (p2 * p2) + 4.0 * (p3 * p3) - 4.0;
-    const double iden = 1.0 / den;
+    const double iden = frcp(den);
     Q[0] = (-((8.0 * (p2 * p2) + 8.0 * (p3 * p3)) * iden - 1.0) * den) * iden;
     Q[1] = (8.0 * p1 * p2 + p3 * a) * iden;
     Q[2] = (8.0 * p1 * p3 - p2 * a) * iden;
@@ -125,7 +155,10 @@ DCOL_HD void make_frame(const DevShape& S, const double th[6], Frame& F) {
     dcm_from_mrp(th[3], th[4], th[5], Q);
     const double o0 = S.r_off[0], o1 = S.r_off[1], o2 = S.r_off[2];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) F.re[k] = th[k] + (Q[3 * k] * o0 + Q[3 * k + 1] * o1 + Q[3 * k + 2] * o2);
+    for (int k = 0; k < 3; ++k) {
+        F.qro[k] = Q[3 * k] * o0 + Q[3 * k + 1] * o1 + Q[3 * k + 2] * o2;
+        F.re[k] = th[k] + F.qro[k];
+    }
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
@@ -143,7 +176,7 @@ DCOL_HD void make_frame(const DevShape& S, const double th[6], Frame& F) {
 DCOL_HD void dcm_jacobian(const double p[3], double dQ[3][9]) {
     const double S = p[0] * p[0] + p[1] * p[1] + p[2] * p[2];
     const double s1 = 1.0 + S;
-    const double iden = 1.0 / (s1 * s1);
+    const double iden = frcp(s1 * s1);
     const double a = 4.0 * S - 4.0;
     const double K[9] = {0.0, p[2], -p[1], -p[2], 0.0, p[0], p[1], -p[0], 0.0};
     double Nm[9];
@@ -153,7 +186,7 @@ DCOL_HD void dcm_jacobian(const double p[3], double dQ[3][9]) {
         for (int c = 0; c < 3; ++c) Nm[3 * r + c] = 8.0 * (p[r] * p[c] - (r == c ? S : 0.0)) + a * K[3 * r + c];
     // K_j = dK/dp_j
     const double Kj[3][9] = {{0, 0, 0, 0, 0, 1, 0, -1, 0}, {0, 0, -1, 0, 0, 0, 1, 0, 0}, {0, 1, 0, -1, 0, 0, 0, 0, 0}};
-    const double is1 = 1.0 / s1;
+    const double is1 = frcp(s1);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
 #pragma unroll
@@ -179,8 +212,8 @@ struct SocNT {
 DCOL_HD void soc_nt(const double* s, const double* z, SocNT& W) {
     const double Jz = z[0] * z[0] - (z[1] * z[1] + z[2] * z[2] + z[3] * z[3]);
     const double Js = s[0] * s[0] - (s[1] * s[1] + s[2] * s[2] + s[3] * s[3]);
-    const double iz = 1.0 / sqrt(Jz);
-    const double is = 1.0 / sqrt(Js);
+    const double iz = frsqrt(Jz);
+    const double is = frsqrt(Js);
     double zb[4], sb[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -188,14 +221,13 @@ DCOL_HD void soc_nt(const double* s, const double* z, SocNT& W) {
         sb[k] = s[k] * is;
     }
     const double dot = zb[0] * sb[0] + zb[1] * sb[1] + zb[2] * sb[2] + zb[3] * sb[3];
-    const double gamma = sqrt((1.0 + dot) * 0.5);
-    const double i2g = 1.0 / (2.0 * gamma);
+    const double i2g = 0.5 * frsqrt((1.0 + dot) * 0.5);   // 1/(2 gamma)
     W.w0 = (sb[0] + zb[0]) * i2g;
 #pragma unroll
     for (int k = 0; k < 3; ++k) W.w1[k] = (sb[k + 1] - zb[k + 1]) * i2g;
-    W.bf = 1.0 / (W.w0 + 1.0);
-    W.eta = (Jz != 0.0) ? sqrt(sqrt(Js / Jz)) : 1.0;   // quirk Q9
-    W.ieta = 1.0 / W.eta;
+    W.bf = frcp(W.w0 + 1.0);
+    W.eta = (Jz != 0.0) ? sqrt(sqrt(Js * frcp(Jz))) : 1.0;   // quirk Q9
+    W.ieta = frcp(W.eta);
 }
 
 // out = W v
@@ -229,8 +261,8 @@ DCOL_HD void soc_prod(const double* u, const double* v, double* out) {
 DCOL_HD void soc_iprod(const double* u, const double* w, double* out) {
     const double rho = u[0] * u[0] - (u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
     const double nu = u[1] * w[1] + u[2] * w[2] + u[3] * w[3];
-    const double irho = 1.0 / rho;
-    const double iu0 = 1.0 / u[0];
+    const double irho = frcp(rho);
+    const double iu0 = frcp(u[0]);
     const double c1 = nu * iu0 - w[0];
     const double c2 = rho * iu0;
     out[0] = irho * (u[0] * w[0] - nu);
@@ -242,11 +274,10 @@ DCOL_HD void soc_iprod(const double* u, const double* w, double* out) {
 DCOL_HD double soc_ls(const double* y, const double* d) {
     const double nu = fmax(y[0] * y[0] - (y[1] * y[1] + y[2] * y[2] + y[3] * y[3]), 1e-25);
     const double zeta = y[0] * d[0] - (y[1] * d[1] + y[2] * d[2] + y[3] * d[3]);
-    const double sn = sqrt(nu);
-    const double isn = 1.0 / sn;
-    const double inu = 1.0 / nu;
+    const double isn = frsqrt(nu);
+    const double inu = isn * isn;
     const double rho0 = zeta * inu;
-    const double coef = (zeta * isn + d[0]) / (y[0] * isn + 1.0);
+    const double coef = (zeta * isn + d[0]) * frcp(y[0] * isn + 1.0);
     double n2 = 0.0;
 #pragma unroll
     for (int k = 1; k < 4; ++k) {
@@ -254,7 +285,7 @@ DCOL_HD double soc_ls(const double* y, const double* d) {
         n2 += r * r;
     }
     const double n1 = sqrt(n2);
-    return (n1 > rho0) ? fmin(1.0, 1.0 / (n1 - rho0)) : 1.0;
+    return (n1 > rho0) ? fmin(1.0, frcp(n1 - rho0)) : 1.0;
 }
 
 // ------------------------------------------------------------------------------------
@@ -478,9 +509,8 @@ struct Solver {
 #pragma unroll
             for (int k = 0; k < j; ++k) d -= F[k][j] * F[k][j];
             ok = ok && (d > 0.0);
-            const double fjj = sqrt(d);
-            F[j][j] = fjj;
-            idg[j] = 1.0 / fjj;
+            idg[j] = frsqrt(d);
+            F[j][j] = d * idg[j];
 #pragma unroll
             for (int c = j + 1; c < N; ++c) {
                 double t = H[j][c];
@@ -641,8 +671,7 @@ struct Solver {
 #pragma unroll
             for (int k = 0; k < OR; ++k) {
                 const double sk = s[k], zk = z[k];
-                const double lam = sqrt(sk * zk);
-                il[k] = 1.0 / lam;
+                il[k] = frsqrt(sk * zk);                  // 1/lambda, lambda = sqrt(s z)
                 if (vort(k)) sz += sk * zk;
                 const double wi = zk * il[k];
                 double g[N];
@@ -718,7 +747,7 @@ struct Solver {
 #pragma unroll
             for (int k = 0; k < M; ++k)
                 if (vrow(k)) rho += (s[k] + aa * dsA[k]) * (z[k] + aa * dzA[k]);
-            rho = R::sum(rho) / sz;
+            rho = R::sum(rho) * frcp(sz);
             const double sc = fmax(0.0, fmin(1.0, rho));
             const double sigma = sc * sc * sc;                      // quirk Q6
             // cp = (W^-1 ds_a) o (W dz_a)
@@ -910,9 +939,7 @@ struct Solver {
     }
 
     // lane part of f_k(theta_k) = sum over rows of primitive k of z_i (G_i(theta_k) x - h_i(theta_k))
-    DCOL_HD double lag_part(const KArgs& A, const DevShape& S, int prim, const double th[6]) const {
-        Frame Fr;
-        make_frame(S, th, Fr);
+    DCOL_HD double lag_part(const KArgs& A, const DevShape& S, int prim, const Frame& Fr) const {
         const double* __restrict__ rows = reinterpret_cast<const double*>(A.rows);
         double acc = 0.0;
 #pragma unroll
@@ -949,21 +976,32 @@ struct Solver {
         return acc;
     }
 
-    // scipy approx_fprime(theta, f, sqrt(eps)) restricted to primitive prim's 6 coordinates
+    // scipy approx_fprime(theta, f, sqrt(eps)) restricted to primitive prim's 6 coordinates.
+    // Translation perturbations keep the rotation: only r_eff = r + Q r_offset moves.
     DCOL_HD void fd_grad_prim(const KArgs& A, const DevShape& S, int prim, const double th0[6], double* g) const {
         const double hstep = 1.4901161193847656e-08;   // sqrt(finfo(float).eps)
-        const double f0 = R::sum(lag_part(A, S, prim, th0));
+        Frame F0;
+        make_frame(S, th0, F0);
+        const double f0 = R::sum(lag_part(A, S, prim, F0));
 #pragma unroll 1
         for (int j = 0; j < 6; ++j) {
-            double th[6];
-#pragma unroll
-            for (int c = 0; c < 6; ++c) th[c] = th0[c];
             double hj = hstep;
             if ((th0[j] + hstep) - th0[j] == 0.0)       // _numdiff: fall back to a relative step
                 hj = hstep * (th0[j] >= 0.0 ? 1.0 : -1.0) * fmax(1.0, fabs(th0[j]));
-            th[j] = th0[j] + hj;
-            const double dxj = th[j] - th0[j];
-            g[j] = (R::sum(lag_part(A, S, prim, th)) - f0) / dxj;
+            const double tj = th0[j] + hj;
+            const double dxj = tj - th0[j];
+            Frame Fj;
+            if (j < 3) {
+                Fj = F0;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) Fj.re[c] = (c == j ? tj : th0[c]) + F0.qro[c];
+            } else {
+                double th[6];
+#pragma unroll
+                for (int c = 0; c < 6; ++c) th[c] = (c == j) ? tj : th0[c];
+                make_frame(S, th, Fj);
+            }
+            g[j] = (R::sum(lag_part(A, S, prim, Fj)) - f0) / dxj;
         }
     }
 
