@@ -121,7 +121,25 @@ struct KArgs {
     double* __restrict__ grad;          // [12][B]
     int32_t* __restrict__ iters;        // [B]
     int32_t* __restrict__ status;       // [B]
+#ifdef DCOL_STAMPS
+    unsigned long long* stamps;         // diagnostic build only (tools/stamp_probe.hip): [B][8]
+#endif
 };
+
+#if defined(DCOL_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+#define DCOL_STAMP(A, pi, q, k)                                                         \
+    do {                                                                                \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        unsigned long long t_;                                                          \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");      \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        if ((q) == 0) (A).stamps[8 * (pi) + (k)] = t_;                                  \
+    } while (0)
+#else
+#define DCOL_STAMP(A, pi, q, k) \
+    do {                        \
+    } while (0)
+#endif
 
 // ------------------------------------------------------------------------------------
 // primitive frames
@@ -977,32 +995,43 @@ struct Solver {
     }
 
     // scipy approx_fprime(theta, f, sqrt(eps)) restricted to primitive prim's 6 coordinates.
-    // Translation perturbations keep the rotation: only r_eff = r + Q r_offset moves.
+    // Translation perturbations keep the rotation: only r_eff = r + Q r_offset moves; the
+    // three rotation perturbations are evaluated together (independent chains, ILP).
     DCOL_HD void fd_grad_prim(const KArgs& A, const DevShape& S, int prim, const double th0[6], double* g) const {
         const double hstep = 1.4901161193847656e-08;   // sqrt(finfo(float).eps)
-        Frame F0;
-        make_frame(S, th0, F0);
-        const double f0 = R::sum(lag_part(A, S, prim, F0));
-#pragma unroll 1
+        double tj[6], dxj[6];
+#pragma unroll
         for (int j = 0; j < 6; ++j) {
             double hj = hstep;
             if ((th0[j] + hstep) - th0[j] == 0.0)       // _numdiff: fall back to a relative step
                 hj = hstep * (th0[j] >= 0.0 ? 1.0 : -1.0) * fmax(1.0, fabs(th0[j]));
-            const double tj = th0[j] + hj;
-            const double dxj = tj - th0[j];
-            Frame Fj;
-            if (j < 3) {
-                Fj = F0;
-#pragma unroll
-                for (int c = 0; c < 3; ++c) Fj.re[c] = (c == j ? tj : th0[c]) + F0.qro[c];
-            } else {
-                double th[6];
-#pragma unroll
-                for (int c = 0; c < 6; ++c) th[c] = (c == j) ? tj : th0[c];
-                make_frame(S, th, Fj);
-            }
-            g[j] = (R::sum(lag_part(A, S, prim, Fj)) - f0) / dxj;
+            tj[j] = th0[j] + hj;
+            dxj[j] = tj[j] - th0[j];
         }
+        Frame F0;
+        make_frame(S, th0, F0);
+        double f[7];
+        f[0] = lag_part(A, S, prim, F0);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            Frame Fj = F0;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) Fj.re[c] = (c == j ? tj[j] : th0[c]) + F0.qro[c];
+            f[1 + j] = lag_part(A, S, prim, Fj);
+        }
+#pragma unroll
+        for (int j = 3; j < 6; ++j) {
+            double th[6];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) th[c] = (c == j) ? tj[j] : th0[c];
+            Frame Fj;
+            make_frame(S, th, Fj);
+            f[1 + j] = lag_part(A, S, prim, Fj);
+        }
+#pragma unroll
+        for (int j = 0; j < 7; ++j) f[j] = R::sum(f[j]);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) g[j] = (f[1 + j] - f[0]) / dxj[j];
     }
 
     // closed-form d/dtheta_k of z'(G(theta)x - h(theta)) (see DESIGN.md "gradient modes"):
@@ -1092,6 +1121,7 @@ DCOL_HD void launder(P& p) {
 
 template <int N, int NSOC, int OMAX, int LPP>
 DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
+    DCOL_STAMP(A, pi, q, 0);
     const int64_t B = A.B;
     const int k1 = A.s1[pi], k2 = A.s2[pi];
     const DevShape& S1 = A.shapes[k1];
@@ -1105,14 +1135,19 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
     Frame F1, F2;
     make_frame(S1, th1, F1);
     make_frame(S2, th2, F2);
+    DCOL_STAMP(A, pi, q, 1);
 
     Solver<N, NSOC, OMAX, LPP> P;
     P.q = q;
     P.assemble(A, S1, S2, F1, F2);
+    DCOL_STAMP(A, pi, q, 2);
     int it = 0;
     int32_t st;
-    if (!P.initialize()) st = ST_NOT_PD;
+    const bool init_ok = P.initialize();
+    DCOL_STAMP(A, pi, q, 3);
+    if (!init_ok) st = ST_NOT_PD;
     else st = P.pdip(A.tol, A.max_iter, &it);
+    DCOL_STAMP(A, pi, q, 4);
 
     const double nan = __builtin_nan("");
     const bool ok = st == ST_OK;
@@ -1148,6 +1183,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
             for (int c = 0; c < 12; ++c) g[c] = nan;
         }
     }
+    DCOL_STAMP(A, pi, q, 5);
     if (q != 0) return;
     A.alpha[pi] = ok ? P.x[3] : nan;
     if (A.iters) A.iters[pi] = it;

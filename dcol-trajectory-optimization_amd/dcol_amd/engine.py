@@ -143,6 +143,38 @@ class Plan:
                    "dcol_plan_run")
         return out
 
+    def bind(self, pose1, pose2, out, tol=DEFAULT_TOL, max_iter=DEFAULT_MAX_ITER, grad="fd", contact=False,
+             stream=None):
+        """Pre-convert every argument of dcol_plan_run once; returns a zero-argument callable
+        that re-launches the solve on the same device buffers (hot loops: ALTRO phases,
+        bench.py).  Validates like run()."""
+        import torch
+        B = self.B
+        dev = torch.device("cuda", self.table.device)
+        for t in (pose1, pose2):
+            if t.dtype != torch.float64 or tuple(t.shape) != (6, B) or not t.is_contiguous() or t.device != dev:
+                raise ValueError(f"poses must be contiguous float64 [6, {B}] on {dev}")
+        flags = grad_flag(grad) | (_lib.CONTACT if contact else 0)
+        if (flags & (_lib.GRAD_FD | _lib.GRAD_ENVELOPE)) and "grad" not in out:
+            raise ValueError("out has no 'grad' buffer")
+        if contact and "contact" not in out:
+            raise ValueError("out has no 'contact' buffer")
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        args = (self.handle, ptr(pose1), ptr(pose2), ctypes.c_double(tol), ctypes.c_int32(max_iter),
+                ctypes.c_int32(flags), ptr(out["alpha"]), ptr(out.get("contact")), ptr(out.get("grad")),
+                ptr(out["iters"]), ptr(out["status"]), ctypes.c_void_p(stream.cuda_stream))
+        fn = _lib.load().dcol_plan_run
+        keep = (self, pose1, pose2, out)
+
+        def launch():
+            rc = fn(*args)
+            if rc:
+                _lib.check(rc, "dcol_plan_run")
+        launch.keep = keep
+        return launch
+
     def __del__(self):
         h = getattr(self, "handle", None)
         if h is not None and h.value:
