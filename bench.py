@@ -109,6 +109,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check", type=int, default=256, help="pairs re-checked against the oracle")
     ap.add_argument("--max-iter", type=int, default=50, help="PDIP iteration cap (diagnostics only; reference: 50)")
+    ap.add_argument("--backend", default=os.environ.get("DCOL_DIST_BACKEND", "nccl"),
+                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo for rehearsals)")
     args = ap.parse_args()
 
     import torch
@@ -116,13 +118,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    ndev = torch.cuda.device_count()
+    local = local % max(ndev, 1)    # rehearsals may run more ranks than devices (gloo)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local)
+    coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
 
     from dcol_amd import Engine, spec_from_arrays
     tab = shape_table()
@@ -164,7 +172,7 @@ def main():
     torch.cuda.synchronize(dev)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if dist is not None:
-        t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, kern_ms], device=coll_dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms_max = float(t[0]), float(t[1])
     else:
@@ -183,7 +191,7 @@ def main():
     value = total / elapsed
     achieved_gbs = BYTES_PER_PAIR * B / (kern_ms * 1e-3) / 1e9
     traffic = read_traffic(os.path.join(REPO, "profiles"))
-    flops_pair = flops_per_pair(iters[status == 0])
+    flops_pair = flops_per_pair(iters[status == 0], args.grad)
     line = {
         "metric": "PDIP proximity+grad pair-solves/sec",
         "value": value,
@@ -231,12 +239,14 @@ def main():
         dist.destroy_process_group()
 
 
-def flops_per_pair(iters):
+def flops_per_pair(iters, grad="fd"):
     """Algorithmic FP64 operation count per pair, poly6 x poly6 (m = 12, n = 4), from the
     hand model of SURVEY.md §8d (each +,-,*,/,sqrt = 1, following pdip.py/NT_scaling.py):
-    assembly 530 + init 777 + iters x 1682 + exit iteration 276 + FD gradient 8485."""
+    assembly 530 + init 777 + iters x 1682 + exit iteration 276 + gradient, where the FD
+    gradient (13 re-assemblies + z'(Gx-h)) is 8485 and the closed-form envelope gradient
+    (w = sum z_i a_i, two DCM Jacobians, three bilinear forms per primitive) is 760."""
     it = float(np.mean(iters)) if len(iters) else 7.0
-    return 530 + 777 + it * 1682 + 276 + 8485
+    return 530 + 777 + it * 1682 + 276 + (8485 if grad == "fd" else 760)
 
 
 if __name__ == "__main__":
