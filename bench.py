@@ -104,7 +104,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--pairs", type=int, default=100_000, help="pairs per GPU")
     ap.add_argument("--grad", choices=["fd", "envelope"], default="fd")
-    ap.add_argument("--cpu-sample", type=int, default=4000)
+    ap.add_argument("--cpu-sample", type=int, default=16000)
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check", type=int, default=256, help="pairs re-checked against the oracle")

@@ -1,0 +1,243 @@
+"""Batched AL-iLQR (ALTRO) driver over the GPU proximity engine.
+
+Same algorithm, parameters, dual/penalty schedule, regularisation rule and printout as the
+reference optimizer (ALTRO.py:365-488); what changes is how the work is issued:
+
+  reference (per knot, per obstacle, Python)      here
+  ---------------------------------------------   ------------------------------------------
+  backward_pass: at every knot, N x n_obs alpha    ONE gradient batch of N x n_obs pairs on
+    solves + N x n_obs gradient solves              the GPU (ObstacleField.evaluate, grad)
+    (ALTRO.py:268-300)                              — its alpha also serves the forward pass's
+                                                    old cost (same trajectory)
+  compute_jacobian per knot (ALTRO.py:77-100)      dcol_altro_jacobians, all knots, native
+  Riccati loop with scipy cho_factor (:304-336)    dcol_altro_backward, native
+  forward_pass: old cost recomputed per line-      old cost from the cached alpha; per trial
+    search trial, rollout + N x n_obs solves        one native rollout + ONE alpha batch
+    (:183-239)
+  AL dual update re-solves N x n_obs (:444-470)    reuses the accepted trial's alpha
+  cost / AL terms per knot (:103-145, :259-300)    vectorised over knots (NumPy)
+
+Every reuse is of a value the reference recomputes from identical inputs, so the
+iterates are the reference's up to floating-point rounding (tests/test_altro.py pins them
+against whole-run fixtures of the reference itself).
+"""
+from __future__ import annotations
+
+import dataclasses
+import logging
+import time
+
+import numpy as np
+
+from . import _native
+from . import systems as _systems
+
+log = logging.getLogger("altro")
+
+
+@dataclasses.dataclass
+class AltroResult:
+    X: np.ndarray                      # [N, nx]
+    U: np.ndarray                      # [N-1, nu]
+    converged: bool
+    iterations: int                    # outer iterations run (backward passes)
+    J: list = dataclasses.field(default_factory=list)
+    delta_J: list = dataclasses.field(default_factory=list)
+    kmax: list = dataclasses.field(default_factory=list)
+    alpha: list = dataclasses.field(default_factory=list)
+    reg: list = dataclasses.field(default_factory=list)      # reg on entry to each iteration
+    rho: list = dataclasses.field(default_factory=list)      # rho on entry to each iteration
+    convio: list = dataclasses.field(default_factory=list)   # (iteration, violation) at each AL update
+    wall_s: float = 0.0
+    prox_s: float = 0.0                # time inside proximity batches (H2D + kernel + D2H)
+    prox_batches: int = 0
+    prox_pairs: int = 0
+
+    @property
+    def ms_per_iter(self) -> float:
+        return 1e3 * self.wall_s / max(self.iterations, 1)
+
+
+class _Timed:
+    """Wraps a constraint evaluator and accounts the time spent in it."""
+
+    def __init__(self, field):
+        self.field = field
+        self.seconds = 0.0
+        self.batches = 0
+        self.pairs = 0
+
+    def __call__(self, poses, grad):
+        t0 = time.perf_counter()
+        out = self.field.evaluate(poses, grad)
+        self.seconds += time.perf_counter() - t0
+        self.batches += 1
+        self.pairs += poses.shape[0] * out[0].shape[1]
+        return out
+
+
+def _masked(dual, h):
+    """Active-set mask of the AL penalty: mu > 0 or h > 0 (ALTRO.py:16-31)."""
+    return ((dual > 0) | (h > 0)).astype(np.float64)
+
+
+class _Problem:
+    """Array views of a reference params dict."""
+
+    def __init__(self, params):
+        self.params = params
+        self.sys = _systems.get(params["system"])
+        self.N, self.nx, self.nu = int(params["N"]), int(params["nx"]), int(params["nu"])
+        self.Q = np.asarray(params["Q"], dtype=np.float64)
+        self.R = np.asarray(params["R"], dtype=np.float64)
+        self.Qf = np.asarray(params["Qf"], dtype=np.float64)
+        self.Xref = np.asarray(params["Xref"], dtype=np.float64).reshape(-1, self.nx)[: self.N]
+        self.Uref = np.asarray(params["Uref"], dtype=np.float64).reshape(-1, self.nu)[: self.N - 1]
+        self.u_max = np.asarray(params["u_max"], dtype=np.float64)
+        self.u_min = np.asarray(params["u_min"], dtype=np.float64)
+        self.model = self.sys.native_model(params)
+        I = np.eye(self.nu)
+        self.Gu = np.vstack([I, -I])                       # d h_u / d u (constant)
+
+    def hu(self, U):
+        return np.concatenate([U - self.u_max, -U + self.u_min], axis=1)
+
+    def cost(self, X, U, hx, hu, mu, mux, lam, rho):
+        """compute_total_cost (ALTRO.py:103-145), terms summed in the reference's order."""
+        dx = X - self.Xref
+        du = U - self.Uref
+        run = 0.5 * np.einsum("ti,ij,tj->t", dx[:-1], self.Q, dx[:-1]) + 0.5 * np.einsum("ti,ij,tj->t", du, self.R, du)
+        mu_mask = _masked(mu, hu)
+        x_mask = _masked(mux, hx)
+        alu = np.einsum("ti,ti->t", mu, hu) + 0.5 * rho * np.einsum("ti,ti,ti->t", hu, mu_mask, hu)
+        alx = np.einsum("ti,ti->t", mux, hx) + 0.5 * rho * np.einsum("ti,ti,ti->t", hx, x_mask, hx)
+        g = X[-1] - self.Xref[-1]
+        tail = [0.5 * dx[-1] @ self.Qf @ dx[-1], alx[-1], lam @ g + 0.5 * rho * (g @ g)]
+        terms = np.concatenate([np.stack([run, alu, alx[:-1]], axis=1).ravel(), tail])
+        return float(np.cumsum(terms)[-1])
+
+
+def _print_iter(itr, J, dJ, kmax, a, reg, rho):
+    if itr % 50 == 0:
+        print("iter     J           ΔJ        |d|         α        reg         ρ")
+        print("---------------------------------------------------------------------")
+    print(f"{itr+1:3d}   {J:10.3e}  {dJ:9.2e}  {kmax:9.2e}  {a:6.4f}   {reg:9.2e}   {rho:9.2e}")
+
+
+def solve(params, X, U, prox=None, engine=None, verbose=True) -> AltroResult:
+    """Run the batched ALTRO on a reference-style problem.
+
+    params/X/U: as returned by altro.systems.<system>.initialize() (or the reference's own
+    initialize_<system>()).  prox: constraint evaluator with
+    ``evaluate(victim_poses [N, 6], grad) -> (alpha [N, n_obs], J [N, n_obs, 12] | None)``;
+    default: an ObstacleField on the GPU (constraints.py).  params['reg'] / ['rho'] /
+    ['X_hist'] / ['U_hist'] are updated in place like the reference does."""
+    t_start = time.perf_counter()
+    P = _Problem(params)
+    N, nx, nu = P.N, P.nx, P.nu
+    X = np.array(X, dtype=np.float64).reshape(N, nx)
+    U = np.array(U, dtype=np.float64).reshape(N - 1, nu)
+    if prox is None:
+        from .constraints import ObstacleField
+        prox = ObstacleField(params["P_vic"], params["P_obs"], N, engine=engine)
+    evaluate = _Timed(prox)
+    ncx = len(params["P_obs"])
+    if int(params.get("ncx", ncx)) != ncx or int(params.get("ncu", 2 * nu)) != 2 * nu:
+        raise AssertionError("ncx / ncu do not match the problem")
+
+    # initial rollout (ALTRO.py:407-409)
+    X, U = _native.rollout(P.model, X, U, np.zeros((N - 1, nu, nx)), np.zeros((N - 1, nu)), 0.0)
+    params.setdefault("X_hist", []).append(X)
+    params.setdefault("U_hist", []).append(U)
+
+    mu = np.zeros((N - 1, 2 * nu))
+    mux = np.zeros((N, ncx))
+    lam = np.zeros(nx)
+    res = AltroResult(X=X, U=U, converged=False, iterations=0)
+    hx_cur = None            # 1 - alpha at the current X, when known from the last accepted trial
+    max_iters = int(params["max_iters"])
+    for itr in range(max_iters):
+        rho, reg = float(params["rho"]), float(params["reg"])   # mutated in place, like the reference
+        res.reg.append(reg)
+        res.rho.append(rho)
+        # ---------------------------------------------------------------- backward pass
+        alpha, Jp = evaluate(P.sys.victim_poses(params, X), True)
+        hx = 1 - alpha
+        Gx = P.sys.state_jacobian(params, X, Jp)                    # [N, ncx, nx]
+        hu = P.hu(U)
+        A, B = _native.jacobians(P.model, X, U)
+        dx = X - P.Xref
+        du = U - P.Uref
+        xm = _masked(mux, hx)
+        um = _masked(mu, hu)
+        lx = dx @ P.Q.T + np.einsum("tci,tc->ti", Gx, mux + rho * (xm * hx))
+        lxx = P.Q + rho * np.einsum("tci,tc,tcj->tij", Gx, xm, Gx)
+        lu = du @ P.R.T + (mu + rho * (um * hu)) @ P.Gu
+        luu = P.R + rho * np.einsum("ci,tc,cj->tij", P.Gu, um, P.Gu)
+        g = X[-1] - P.Xref[-1]
+        VxT = P.Qf @ dx[-1] + Gx[-1].T @ (mux[-1] + rho * (xm[-1] * hx[-1])) + (lam + rho * g)
+        VxxT = P.Qf + rho * (Gx[-1].T * xm[-1]) @ Gx[-1] + rho * np.eye(nx)
+        K, k, dJ = _native.backward(A, B, lx[:-1], lu, lxx[:-1], luu, VxT, VxxT, reg)
+        # ---------------------------------------------------------------- forward pass
+        old = P.cost(X, U, hx, hu, mu, mux, lam, rho)
+        a, J, accepted = 1.0, old, False
+        for _ in range(int(params["max_linesearch_iters"])):
+            Xn, Un = _native.rollout(P.model, X, U, K, k, a)
+            an, _ = evaluate(P.sys.victim_poses(params, Xn), False)
+            hxn = 1 - an
+            new = P.cost(Xn, Un, hxn, P.hu(Un), mu, mux, lam, rho)
+            if new < old:
+                X, U, J, accepted, hx_cur = Xn, Un, new, True, hxn
+                break
+            a *= 0.5
+        if not accepted:
+            log.warning("Forward pass failed to reduce cost after line search, increasing reg")
+            a, hx_cur = 0.0, hx
+        params["X_hist"].append(X)
+        params["U_hist"].append(U)
+        # ---------------------------------------------------- regularisation (ALTRO.py:51-74)
+        if a == 0.0:
+            if reg == params["reg_max"]:
+                raise ValueError("Regularization parameter reached maximum value.")
+            params["reg"] = min(params["reg_max"], reg * 10)
+        elif a == 1.0:
+            params["reg"] = max(params["reg_min"], reg / 10)
+        kmax = float(np.max(np.linalg.norm(k, axis=1))) if len(k) else 0.0
+        kmax = max(0.0, kmax)
+        res.J.append(J)
+        res.delta_J.append(dJ)
+        res.kmax.append(kmax)
+        res.alpha.append(a)
+        res.iterations = itr + 1
+        if verbose:
+            _print_iter(itr, J, dJ, kmax, a, params["reg"], rho)
+        # ------------------------------------------------------ AL update (ALTRO.py:444-481)
+        if a > 0 and kmax < params["atol"]:
+            hu = P.hu(U)
+            mu = np.maximum(0, mu + rho * (_masked(mu, hu) * hu))
+            mux = np.maximum(0, mux + rho * (_masked(mux, hx_cur) * hx_cur))
+            g = X[-1] - P.Xref[-1]
+            lam = lam + rho * g
+            convio = max(float(np.max(np.abs(hu + np.abs(hu)))) if hu.size else 0.0,
+                         float(np.max(np.abs(hx_cur + np.abs(hx_cur)))) if hx_cur.size else 0.0,
+                         float(np.max(np.abs(g))))
+            res.convio.append((itr, convio))
+            if convio < params["convio_tol"]:
+                log.info(f"Convergence reached in {itr} iterations.")
+                res.converged = True
+                break
+            log.info(f"convio: {convio}, increasing penalty parameter")
+            params["rho"] = rho * params["phi"]
+    else:
+        log.info("iLQR optimization complete without convergence")
+    res.X, res.U = X, U
+    res.wall_s = time.perf_counter() - t_start
+    res.prox_s, res.prox_batches, res.prox_pairs = evaluate.seconds, evaluate.batches, evaluate.pairs
+    return res
+
+
+def ALTRO(params, X, U, prox=None, engine=None, verbose=True):
+    """Drop-in for the reference's ALTRO(params, X, U) (ALTRO.py:365-488): returns the
+    optimised (X, U) as lists of per-knot arrays."""
+    r = solve(params, X, U, prox=prox, engine=engine, verbose=verbose)
+    return [x.copy() for x in r.X], [u.copy() for u in r.U]

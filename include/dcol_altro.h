@@ -1,0 +1,86 @@
+/*
+ * dcol_altro.h — C-ABI of the native host kernels of the batched ALTRO constraint driver
+ * (SURVEY.md §8 f1/f3).  The proximity solves themselves go through dcol.h on the GPU;
+ * this library holds the sequential, knot-coupled host work around them, which the
+ * reference runs as per-knot NumPy calls:
+ *
+ *   reference                                                 replaced by
+ *   ------------------------------------------------------   ---------------------------------
+ *   systems/<sys>.py discrete_dynamics (RK4 of dynamics)      dcol_altro_dynamics()
+ *     piano_mover.py:7-47, cluttered_hallway_quadrotor.py:      (batched over states)
+ *     19-105, cone_through_wall.py:19-86
+ *   ALTRO.py compute_jacobian (forward differences,           dcol_altro_jacobians()
+ *     delta 1e-6) called per knot at ALTRO.py:289-290           (all knots in one call)
+ *   ALTRO.py backward_pass Riccati recursion :304-336          dcol_altro_backward()
+ *     (Quu = luu + B'(Vxx+reg I)B, scipy cho_factor/solve)
+ *   ALTRO.py forward_pass rollout :214-217                     dcol_altro_rollout()
+ *     (U - K(Xn - X) - a k, then discrete_dynamics)
+ *
+ * Row-major float64 arrays; plain pointers and sizes; no allocation visible to callers.
+ * Every entry point returns DCOL_ALTRO_OK or a negative DCOL_ALTRO_ERR_*.
+ */
+#ifndef DCOL_ALTRO_H
+#define DCOL_ALTRO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCOL_ALTRO_ABI_VERSION 1
+#define DCOL_ALTRO_MAX_NX 16
+#define DCOL_ALTRO_MAX_NU 8
+
+enum dcol_altro_system {
+    DCOL_SYS_PIANO = 0,     /* planar rigid body, x = [r(2) v(2) theta omega], u (3)       */
+    DCOL_SYS_QUADROTOR = 1, /* x = [r v p(MRP) w] (12), u = rotor speeds (4)                */
+    DCOL_SYS_RIGID = 2      /* force/torque-actuated rigid body (coneThroughWall), u (6)    */
+};
+
+enum dcol_altro_error {
+    DCOL_ALTRO_OK = 0,
+    DCOL_ALTRO_ERR_ARG = -1,    /* bad pointer / size / system id                             */
+    DCOL_ALTRO_ERR_NOT_PD = -2  /* Quu not positive definite (scipy cho_factor LinAlgError)    */
+};
+
+/* Physical constants of a model.  Fields a system does not use are ignored. */
+typedef struct dcol_altro_model {
+    int32_t system; /* enum dcol_altro_system                                                */
+    int32_t nx, nu;
+    double dt;          /* RK4 step                                                            */
+    double mass;        /* QUADROTOR / RIGID                                                   */
+    double inertia[9];  /* QUADROTOR / RIGID, row-major 3x3 (solved with partial pivoting)     */
+    double gravity[3];  /* QUADROTOR                                                           */
+    double arm, kf, km; /* QUADROTOR: arm length L, thrust and torque coefficients             */
+    double u_scale;     /* PIANO: angular acceleration = u[2] / u_scale (reference: 100)       */
+} dcol_altro_model;
+
+int32_t dcol_altro_abi_version(void);
+
+/* Xn[i] = RK4(X[i], U[i]) for i < M (independent states).  X [M, nx], U [M, nu]. */
+int dcol_altro_dynamics(const dcol_altro_model* m, int64_t M, const double* X, const double* U, double* Xn);
+
+/* Forward-difference Jacobians of the discrete dynamics at knots t < T:
+ * A[t] = d x_{t+1} / d x_t  [T, nx, nx],  B[t] = d x_{t+1} / d u_t  [T, nx, nu]. */
+int dcol_altro_jacobians(const dcol_altro_model* m, int64_t T, const double* X, const double* U, double delta,
+                         double* A, double* B);
+
+/* Riccati recursion of the regularised AL-iLQR backward pass for knots T-1 .. 0, from the
+ * terminal cost-to-go (VxT [nx], VxxT [nx, nx]).  Per knot: A [nx,nx], B [nx,nu],
+ * lx [nx], lu [nu], lxx [nx,nx], luu [nu,nu].  Outputs gains K [T, nu, nx], k [T, nu],
+ * the expected decrease sum_t Qu'k in *dJ.  On DCOL_ALTRO_ERR_NOT_PD, *fail_knot = t. */
+int dcol_altro_backward(int64_t T, int32_t nx, int32_t nu, const double* A, const double* B, const double* lx,
+                        const double* lu, const double* lxx, const double* luu, const double* VxT,
+                        const double* VxxT, double reg, double* K, double* k, double* dJ, int64_t* fail_knot);
+
+/* Closed-loop rollout: Un[t] = U[t] - K[t](Xn[t] - X[t]) - a k[t];  Xn[t+1] = RK4(Xn[t], Un[t]),
+ * Xn[0] = X[0], t < T.  X [T+1, nx], U [T, nu]. */
+int dcol_altro_rollout(const dcol_altro_model* m, int64_t T, const double* X, const double* U, const double* K,
+                       const double* k, double a, double* Xn, double* Un);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DCOL_ALTRO_H */

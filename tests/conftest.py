@@ -62,3 +62,15 @@ def engine():
         pytest.skip("no GPU")
     from dcol_amd import Engine
     return Engine(device=0)
+
+
+def _ensure_built():
+    """Build lib/libdcol.so and lib/libdcol_altro.so in-tree if a fresh checkout lacks them
+    (hipcc cross-compiles for gfx950 without a GPU)."""
+    import subprocess
+    libs = [os.path.join(PKG, "lib", n) for n in ("libdcol.so", "libdcol_altro.so")]
+    if not all(os.path.exists(p) for p in libs):
+        subprocess.run(["make", "-C", os.path.join(PKG, "csrc"), "-j8", "-s"], check=True)
+
+
+_ensure_built()

@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""Generate whole-run ALTRO fixtures by running the reference optimizer in this container.
+
+For each system the reference's ALTRO (ALTRO.py:365-488) is run unchanged on the
+reference's own initial guess; its module-level backward_pass / forward_pass are wrapped
+to record, per outer iteration: reg and rho on entry, delta_J and max|k| from the backward
+pass (ALTRO.py:242-338, :50-58 of calc_max_k), the line-search step alpha and cost J
+from the forward pass (ALTRO.py:183-239).  The final trajectory and the problem's own
+inputs (initial controls, obstacle poses) are stored too, so tests/ can rerun the batched
+driver on identical inputs without the reference.
+
+Plotting (utils/plots.py) is replaced by no-ops: it draws figures only and feeds nothing
+back into the optimization.  The quadrotor system imports h5py at module level
+(cluttered_hallway_quadrotor.py:2), which this image lacks, so only its initial controls
+and the decoded polytopes.jld2 arrays are stored (from gen_golden.jld2_polytopes), not a
+whole-run trace.
+
+Usage (cwd anywhere; writes tests/golden/altro/altro_<system>.npz and
+dcol-trajectory-optimization_amd/altro/data/initial_guess.npz):
+    PYTHONDONTWRITEBYTECODE=1 python3 tests/golden/gen_altro.py [piano_mover coneThroughWall]
+"""
+import ast
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+DATA = os.path.join(REPO, "dcol-trajectory-optimization_amd", "altro", "data")
+sys.path.insert(0, REF)
+sys.path.insert(0, HERE)
+
+
+def literal_controls(path, fn_name):
+    """The initial control guess the reference hard-codes in `fn_name` (a numeric literal
+    passed to np.array), read as data with ast.literal_eval — no reference code runs."""
+    tree = ast.parse(open(path).read())
+    for node in ast.walk(tree):
+        if isinstance(node, ast.FunctionDef) and node.name == fn_name:
+            for sub in ast.walk(node):
+                if (isinstance(sub, ast.Assign) and len(sub.targets) == 1 and getattr(sub.targets[0], "id", "") == "U"
+                        and isinstance(sub.value, ast.Call) and sub.value.args
+                        and isinstance(sub.value.args[0], ast.List)):
+                    return np.array(ast.literal_eval(sub.value.args[0]), dtype=np.float64)
+    raise RuntimeError(f"no literal U in {fn_name}")
+
+
+def initial_guess():
+    from gen_golden import jld2_polytopes
+    jl = jld2_polytopes()
+    out = dict(piano_mover_U=literal_controls(os.path.join(REF, "systems", "piano_mover.py"), "initialize_piano_mover"),
+               quadrotor_U=literal_controls(os.path.join(REF, "systems", "cluttered_hallway_quadrotor.py"),
+                                            "initialize_quadrotor"),
+               **{f"jld2_{k}": v for k, v in jl.items()})
+    os.makedirs(DATA, exist_ok=True)
+    np.savez(os.path.join(DATA, "initial_guess.npz"), **out)
+    print("initial guess:", {k: v.shape for k, v in out.items()})
+
+
+def run_system(name):
+    import ALTRO as ref_altro
+    for k in ("plot_trajectories", "plot_cost", "plot_regularization"):
+        setattr(ref_altro, k, lambda *a, **kw: None)
+    if name == "piano_mover":
+        from systems.piano_mover import initialize_piano_mover as init
+    elif name == "coneThroughWall":
+        from systems.cone_through_wall import initialize_coneThroughWall as init
+    else:
+        raise SystemExit(f"unsupported system {name}")
+    rec = dict(reg=[], rho=[], delta_J=[], kmax=[], alpha=[], J=[])
+    bp, fp = ref_altro.backward_pass, ref_altro.forward_pass
+
+    def backward(params, X, U, mu, mux, lambd, mod):
+        rec["reg"].append(params["reg"])
+        rec["rho"].append(params["rho"])
+        gains, dJ = bp(params, X, U, mu, mux, lambd, mod)
+        rec["delta_J"].append(float(dJ))
+        rec["kmax"].append(max(float(np.linalg.norm(g[1])) for g in gains))
+        return gains, dJ
+
+    def forward(params, X, U, mu, mux, lambd, gains, itr, mod):
+        X, U, a, J = fp(params, X, U, mu, mux, lambd, gains, itr, mod)
+        rec["alpha"].append(float(a))
+        rec["J"].append(float(J))
+        return X, U, a, J
+
+    ref_altro.backward_pass, ref_altro.forward_pass = backward, forward
+    params, X, U = init()
+    X0 = np.array(X, dtype=np.float64)
+    U0 = np.array(U, dtype=np.float64)
+    t0 = time.time()
+    Xf, Uf = ref_altro.ALTRO(params, X, U)
+    wall = time.time() - t0
+    ref_altro.backward_pass, ref_altro.forward_pass = bp, fp
+    out = {k: np.array(v) for k, v in rec.items()}
+    out.update(X0=X0, U0=U0, X=np.array(Xf), U=np.array(Uf), rho_final=params["rho"], reg_final=params["reg"],
+               iterations=len(rec["J"]), wall_s=wall,
+               obs_r=np.array([np.asarray(o.r, dtype=np.float64) for o in params["P_obs"]]),
+               obs_p=np.array([np.asarray(o.p, dtype=np.float64) for o in params["P_obs"]]))
+    os.makedirs(os.path.join(HERE, "altro"), exist_ok=True)
+    np.savez(os.path.join(HERE, "altro", f"altro_{name}.npz"), **out)
+    print(f"{name}: {len(rec['J'])} outer iterations, J {rec['J'][-1]:.6e}, wall {wall:.1f} s")
+
+
+def main():
+    names = sys.argv[1:] or ["piano_mover", "coneThroughWall"]
+    initial_guess()
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as tmp:
+        os.chdir(tmp)          # utils/plots.py writes result_images/ relative to cwd
+        try:
+            for n in names:
+                run_system(n)
+        finally:
+            os.chdir(cwd)
+
+
+if __name__ == "__main__":
+    main()
