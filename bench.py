@@ -109,6 +109,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check", type=int, default=256, help="pairs re-checked against the oracle")
     ap.add_argument("--max-iter", type=int, default=50, help="PDIP iteration cap (diagnostics only; reference: 50)")
+    ap.add_argument("--no-altro", action="store_true", help="skip the ALTRO wall-clock section")
     ap.add_argument("--backend", default=os.environ.get("DCOL_DIST_BACKEND", "nccl"),
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo for rehearsals)")
     args = ap.parse_args()
@@ -231,12 +232,45 @@ def main():
                       <= 1e-5 * np.maximum(np.abs(ref["grad"][ok]).max(1), 1))
         line["parity_check"] = {"pairs": int(n), "status_equal": bool(np.array_equal(status[:n], ref["status"])),
                                 "alpha_ok": bool(a_ok), "grad_ok": bool(g_ok)}
+    if world == 1 and not args.no_altro:
+        line["altro"] = altro_section()
     if world == 1 and not args.no_cpu:
         workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
         line["cpu_baseline"] = cpu_baseline(tab, s1, s2, p1, p2, args.cpu_sample, workers)
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+# Whole-run ALTRO wall-clock of the reference on the same problems: the
+# Python reference measured in the build container (seconds, outer iterations) and the
+# Julia DifferentiableCollisions.jl numbers of Report.pdf Table 5.
+ALTRO_REFERENCE = {"piano_mover": {"python_s": 51.76, "iterations": 35, "julia_s": 0.445},
+                   "coneThroughWall": {"python_s": 166.04, "iterations": 37, "julia_s": 0.866},
+                   "quadrotor": {"python_s": 1887.9, "iterations": 60, "julia_s": 6.98}}
+
+
+def altro_section():
+    """Second metric of BASELINE.json: ALTRO iteration wall-clock.  Each reference problem
+    is solved end to end by the batched driver (altro/), constraints on this GPU; the
+    optimizer loop is timed (set-up — shape table, plan, code-object load — excluded and
+    reported separately)."""
+    import logging
+    from altro import solve, systems
+    logging.getLogger("altro").setLevel(logging.WARNING)
+    out = {"metric": "ALTRO iter wall-clock", "unit": "ms/iter", "higher_is_better": False, "systems": {}}
+    for name, ref in ALTRO_REFERENCE.items():
+        params, X, U = systems.initialize(name)
+        r = solve(params, X, U, verbose=False)
+        out["systems"][name] = {
+            "converged": r.converged, "iterations": r.iterations, "reference_iterations": ref["iterations"],
+            "ms_per_iter": r.ms_per_iter, "wall_s": r.wall_s, "setup_s": r.setup_s,
+            "prox_ms_per_iter": 1e3 * r.prox_s / max(r.iterations, 1), "prox_batches": r.prox_batches,
+            "pairs_per_batch": r.prox_pairs // max(r.prox_batches, 1),
+            "reference_python_ms_per_iter": 1e3 * ref["python_s"] / ref["iterations"],
+            "julia_ms_per_iter": 1e3 * ref["julia_s"] / ref["iterations"],
+            "speedup_vs_python": ref["python_s"] / r.wall_s, "speedup_vs_julia": ref["julia_s"] / r.wall_s}
+    return out
 
 
 def flops_per_pair(iters, grad="fd"):

@@ -18,7 +18,7 @@ def main():
     params, X, U = systems.initialize(args.system)
     r = solve(params, X, U, verbose=not args.quiet)
     print(json.dumps({"system": args.system, "converged": r.converged, "iterations": r.iterations,
-                      "wall_s": round(r.wall_s, 4), "ms_per_iter": round(r.ms_per_iter, 3),
+                      "wall_s": round(r.wall_s, 4), "setup_s": round(r.setup_s, 4), "ms_per_iter": round(r.ms_per_iter, 3),
                       "prox_s": round(r.prox_s, 4), "prox_batches": r.prox_batches, "prox_pairs": r.prox_pairs,
                       "J_final": r.J[-1] if r.J else None}))
 

@@ -240,8 +240,10 @@ int dcol_altro_jacobians(const dcol_altro_model* m, int64_t T, const double* X, 
                          double* A, double* B) {
     if (!model_ok(m) || T < 0 || (T > 0 && (!X || !U || !A || !B)) || !(delta != 0)) return DCOL_ALTRO_ERR_ARG;
     const int nx = m->nx, nu = m->nu;
-    double f0[MX], f1[MX], xp[MX], up[MU];
+    // knots are independent: spread them over the host cores for the larger problems
+#pragma omp parallel for schedule(static) if (T * (nx + nu) >= 512)
     for (int64_t t = 0; t < T; ++t) {
+        double f0[MX], f1[MX], xp[MX], up[MU];
         const double* x = X + t * nx;
         const double* u = U + t * nu;
         double* At = A + t * nx * nx;

@@ -79,6 +79,10 @@ struct dcol_table {
     std::mutex mu;
     void* stage = nullptr;
     size_t stage_bytes = 0;
+    // side streams for the concurrent variant launches of mixed plans (created on first use)
+    std::mutex side_mu;
+    hipStream_t side[kSideStreams] = {};
+    bool side_ready = false;
 };
 
 struct Launch {
@@ -86,6 +90,7 @@ struct Launch {
     int N, nsoc, omax, lpp;
     int32_t code;   // reject status
     int64_t slot0, n;
+    int lane = 0;   // 0 = caller's stream, 1..kSideStreams = table side stream
 };
 
 struct dcol_plan {
@@ -96,6 +101,14 @@ struct dcol_plan {
     int32_t* d_perm = nullptr;   // nullptr when the whole batch is one variant
     bool owns = false;           // device arrays owned (false: views into table staging)
     std::vector<Launch> launches;
+    int lanes = 1;               // streams the launches are spread over (1 = serial)
+    hipEvent_t fork = nullptr;   // recorded on the caller's stream, awaited by the side streams
+    hipEvent_t join[kSideStreams] = {};
+    ~dcol_plan() {
+        if (fork) (void)hipEventDestroy(fork);
+        for (hipEvent_t& e : join)
+            if (e) (void)hipEventDestroy(e);
+    }
 };
 
 namespace {
@@ -173,6 +186,8 @@ int dcol_table_destroy(dcol_table* t) {
     if (t->d_shapes) (void)hipFree(t->d_shapes);
     if (t->d_rows) (void)hipFree(t->d_rows);
     if (t->stage) (void)hipFree(t->stage);
+    if (t->side_ready)
+        for (hipStream_t s : t->side) (void)hipStreamDestroy(s);
     delete t;
     return DCOL_SUCCESS;
 }
@@ -202,6 +217,8 @@ int dcol_pair_dims(const dcol_table* t, int32_t s1, int32_t s2, int32_t* m, int3
 }  // extern "C"
 
 namespace {
+void assign_lanes(dcol_plan* p);
+
 // Classify + bucket (counting sort by variant key).  Fills p->launches and the slot->pair
 // permutation; returns DCOL_SUCCESS or an error.
 int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, dcol_plan* p,
@@ -234,6 +251,57 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
         perm.insert(perm.end(), kv.second.begin(), kv.second.end());
         p->launches.push_back(L);
     }
+    assign_lanes(p);
+    return DCOL_SUCCESS;
+}
+
+// Mixed batches (e.g. an ALTRO phase: one victim against spheres, cylinders, capsules,
+// cones, polytopes) split into several small variant launches, each far too small to fill
+// the chip; run back to back their latencies add up.  Spread them over the caller's stream
+// plus up to kSideStreams side streams (fork/join through events) — longest-first greedy on
+// a cost estimate (waves x per-pair work), reject launches stay on the caller's stream.
+void assign_lanes(dcol_plan* p) {
+    int solves = 0;
+    for (const Launch& L : p->launches) solves += L.kind == 0;
+    p->lanes = 1;
+    if (solves < 2) return;
+    const int lanes = std::min(solves, kSideStreams + 1);
+    std::vector<int> order;
+    std::vector<double> cost(p->launches.size(), 0.0);
+    for (size_t i = 0; i < p->launches.size(); ++i) {
+        const Launch& L = p->launches[i];
+        if (L.kind != 0) continue;
+        const double waves = std::ceil((double)L.n * L.lpp / 64.0);
+        cost[i] = waves * (double)(L.omax + 4 * L.nsoc + 2 * L.N) * (8.0 / L.lpp);
+        order.push_back((int)i);
+    }
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+    std::vector<double> load(lanes, 0.0);
+    for (int i : order) {
+        const int l = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        p->launches[i].lane = l;
+        load[l] += cost[i];
+    }
+    p->lanes = lanes;
+}
+
+int ensure_fanout(const dcol_table* tc, dcol_plan* p) {
+    if (p->lanes <= 1) return DCOL_SUCCESS;
+    dcol_table* t = const_cast<dcol_table*>(tc);
+    DeviceGuard g(t->device);
+    {
+        std::lock_guard<std::mutex> lk(t->side_mu);
+        if (!t->side_ready) {
+            for (int i = 0; i < kSideStreams; ++i) {
+                hipError_t e = hipStreamCreateWithFlags(&t->side[i], hipStreamNonBlocking);
+                if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("side stream: ") + hipGetErrorString(e));
+            }
+            t->side_ready = true;
+        }
+    }
+    hipError_t e = hipEventCreateWithFlags(&p->fork, hipEventDisableTiming);
+    for (int i = 0; e == hipSuccess && i < p->lanes - 1; ++i) e = hipEventCreateWithFlags(&p->join[i], hipEventDisableTiming);
+    if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("fan-out events: ") + hipGetErrorString(e));
     return DCOL_SUCCESS;
 }
 }  // namespace
@@ -269,6 +337,11 @@ int dcol_plan_create(const dcol_table* t, int64_t B, const int32_t* s1, const in
     if (e != hipSuccess) {
         dcol_plan_destroy(p);
         return fail(DCOL_ERR_HIP, std::string("dcol_plan_create: ") + hipGetErrorString(e));
+    }
+    rc = ensure_fanout(t, p);
+    if (rc != DCOL_SUCCESS) {
+        dcol_plan_destroy(p);
+        return rc;
     }
     *out = p;
     return DCOL_SUCCESS;
@@ -321,19 +394,34 @@ int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, 
     a.grad = grad;
     a.iters = iters;
     a.status = status;
+    const bool fan = p->lanes > 1 && p->fork;
+    hipError_t e = hipSuccess;
+    if (fan) {
+        e = hipEventRecord(p->fork, st);
+        for (int l = 1; e == hipSuccess && l < p->lanes; ++l) e = hipStreamWaitEvent(t->side[l - 1], p->fork, 0);
+        if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_plan_run fork: ") + hipGetErrorString(e));
+    }
     for (const Launch& L : p->launches) {
         a.slot0 = L.slot0;
         a.n = L.n;
-        hipError_t e;
+        hipStream_t ls = (fan && L.lane > 0) ? t->side[L.lane - 1] : st;
         if (L.kind == 1) {
             const int64_t grid = (L.n + kBlock - 1) / kBlock;
-            hipLaunchKernelGGL(reject_kernel, dim3(grid), dim3(kBlock), 0, st, a, L.code);
+            hipLaunchKernelGGL(reject_kernel, dim3(grid), dim3(kBlock), 0, ls, a, L.code);
             e = hipGetLastError();
         } else {
-            e = launch_variant(L.N, L.nsoc, L.omax, L.lpp, a, st);
+            e = launch_variant(L.N, L.nsoc, L.omax, L.lpp, a, ls);
         }
-        if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_plan_run launch: ") + hipGetErrorString(e));
+        if (e != hipSuccess) break;
     }
+    if (fan) {   // join even after a failed launch, so the side streams never run ahead
+        for (int l = 1; l < p->lanes; ++l) {
+            hipError_t j = hipEventRecord(p->join[l - 1], t->side[l - 1]);
+            if (j == hipSuccess) j = hipStreamWaitEvent(st, p->join[l - 1], 0);
+            if (e == hipSuccess) e = j;
+        }
+    }
+    if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_plan_run launch: ") + hipGetErrorString(e));
     return DCOL_SUCCESS;
 }
 
@@ -349,6 +437,8 @@ int dcol_prox_batch_host(const dcol_table* tc, int64_t B, const int32_t* s1, con
     dcol_plan p;   // transient, device arrays are views into the table's staging buffer
     std::vector<int32_t> perm;
     int rc = bucket_pairs(t, B, s1, s2, &p, perm);
+    if (rc != DCOL_SUCCESS) return rc;
+    rc = ensure_fanout(t, &p);
     if (rc != DCOL_SUCCESS) return rc;
     DeviceGuard g(t->device);
     // staging: doubles pose1[6B] pose2[6B] | alpha[B] contact[3B] grad[12B] ; ints s1 s2 perm iters status
