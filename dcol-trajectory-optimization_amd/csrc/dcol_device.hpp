@@ -1201,8 +1201,13 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
 // LPP lanes per pair; slots [slot0, slot0+n) of the plan's permutation (or identity).
 // The n*LPP threads of a launch are contiguous, so a group never straddles the tail.
 // WPS = minimum waves per SIMD requested from the register allocator (variants.py).
+#ifndef DCOL_BLOCK
+#define DCOL_BLOCK 64
+#endif
+constexpr int kSolveBlock = DCOL_BLOCK;
+
 template <int N, int NSOC, int OMAX, int LPP, int WPS>
-__global__ void __launch_bounds__(256, WPS) prox_kernel(KArgs A) {
+__global__ void __launch_bounds__(kSolveBlock, WPS) prox_kernel(KArgs A) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t slot = t / LPP;
     const int q = (int)(t % LPP);

@@ -4,7 +4,7 @@
 #include "dcol_device.hpp"
 
 namespace dcol {
-constexpr int kBlock = 256;   // 4 waves; one lane per pair
+constexpr int kBlock = kSolveBlock;   // threads per workgroup of the solve kernel
 constexpr int kSideStreams = 3;   // extra streams for concurrent variant launches (4 HW queues)
 hipError_t launch_n4(int nsoc, int omax, int lpp, const KArgs& args, hipStream_t stream);
 hipError_t launch_n5(int nsoc, int omax, int lpp, const KArgs& args, hipStream_t stream);

@@ -93,9 +93,9 @@ int main(int argc, char** argv) {
     a.B = B; a.slot0 = 0; a.n = B; a.tol = 1e-6; a.max_iter = 50; a.flags = flags;
     a.alpha = dal; a.contact = nullptr; a.grad = dgr; a.iters = dit; a.status = dst; a.stamps = dstamp;
     constexpr int LPP = 2;
-    const int64_t grid = (B * LPP + 255) / 256;
+    const int64_t grid = (B * LPP + kSolveBlock - 1) / kSolveBlock;
     for (int rep = 0; rep < 3; ++rep) {
-        hipLaunchKernelGGL((prox_kernel<4, 0, 12, LPP, 2>), dim3(grid), dim3(256), 0, 0, a);
+        hipLaunchKernelGGL((prox_kernel<4, 0, 12, LPP, 2>), dim3(grid), dim3(kSolveBlock), 0, 0, a);
         CK(hipDeviceSynchronize());
     }
     std::vector<unsigned long long> st(8 * B);
