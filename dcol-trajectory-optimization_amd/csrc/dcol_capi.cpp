@@ -117,6 +117,8 @@ hipError_t launch_variant(int N, int nsoc, int omax, int lpp, const KArgs& a, hi
     if (N == 4) return launch_n4(nsoc, omax, lpp, a, st);
     if (N == 5) return launch_n5(nsoc, omax, lpp, a, st);
     if (N == 6) return launch_n6(nsoc, omax, lpp, a, st);
+    if (N == 7) return launch_n7(nsoc, omax, lpp, a, st);
+    if (N == 8) return launch_n8(nsoc, omax, lpp, a, st);
     return hipErrorInvalidValue;
 }
 
@@ -222,14 +224,14 @@ void assign_lanes(dcol_plan* p);
 // Classify + bucket (counting sort by variant key).  Fills p->launches and the slot->pair
 // permutation; returns DCOL_SUCCESS or an error.
 int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, dcol_plan* p,
-                 std::vector<int32_t>& perm) {
+                 std::vector<int32_t>& perm, bool case4) {
     const int32_t ns = (int32_t)t->shapes.size();
     using Key = std::tuple<int, int, int, int, int, int>;   // kind, N, nsoc, omax, lpp, code
     std::map<Key, std::vector<int32_t>> groups;
     for (int64_t i = 0; i < B; ++i) {
         if (s1[i] < 0 || s1[i] >= ns || s2[i] < 0 || s2[i] >= ns)
             return fail(DCOL_ERR_ARG, "shape id out of range at pair " + std::to_string(i));
-        PairClass c = classify(t->shapes[s1[i]], t->shapes[s2[i]]);
+        PairClass c = classify(t->shapes[s1[i]], t->shapes[s2[i]], case4);
         Key k = c.status == DCOL_OK ? Key{0, c.N, c.nsoc, c.omax, c.lpp, 0} : Key{1, 0, 0, 0, 0, c.status};
         groups[k].push_back((int32_t)i);
     }
@@ -309,13 +311,19 @@ int ensure_fanout(const dcol_table* tc, dcol_plan* p) {
 extern "C" {
 
 int dcol_plan_create(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, dcol_plan** out) {
+    return dcol_plan_create_ex(t, B, s1, s2, 0, out);
+}
+
+int dcol_plan_create_ex(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, int32_t options,
+                        dcol_plan** out) {
     if (!t || !out || B < 0 || (B > 0 && (!s1 || !s2))) return fail(DCOL_ERR_ARG, "dcol_plan_create: bad arguments");
+    if (options & ~DCOL_PLAN_CASE4) return fail(DCOL_ERR_ARG, "dcol_plan_create_ex: unknown option bits");
     if (B > INT32_MAX) return fail(DCOL_ERR_ARG, "dcol_plan_create: B exceeds 2^31-1");
     *out = nullptr;
     auto* p = new (std::nothrow) dcol_plan();
     if (!p) return fail(DCOL_ERR_NOMEM, "host allocation failed");
     std::vector<int32_t> perm;
-    int rc = bucket_pairs(t, B, s1, s2, p, perm);
+    int rc = bucket_pairs(t, B, s1, s2, p, perm, (options & DCOL_PLAN_CASE4) != 0);
     if (rc != DCOL_SUCCESS) {
         delete p;
         return rc;
@@ -436,7 +444,7 @@ int dcol_prox_batch_host(const dcol_table* tc, int64_t B, const int32_t* s1, con
     std::lock_guard<std::mutex> lk(t->mu);
     dcol_plan p;   // transient, device arrays are views into the table's staging buffer
     std::vector<int32_t> perm;
-    int rc = bucket_pairs(t, B, s1, s2, &p, perm);
+    int rc = bucket_pairs(t, B, s1, s2, &p, perm, (flags & DCOL_CASE4) != 0);
     if (rc != DCOL_SUCCESS) return rc;
     rc = ensure_fanout(t, &p);
     if (rc != DCOL_SUCCESS) return rc;

@@ -408,10 +408,20 @@ struct Solver {
     double s[M], z[M], r[M];   // slack, dual, primal residual G x - h
     double x[N];
     int q, o1, o, deg;
+    int xo2;                   // first extra column of primitive 2 minus 4: S1.n_extra for a
+                               // case-4 pair (both primitives have extras; opt-in extension),
+                               // else 0 (combine_problem_matrices.py cases 1-3)
     bool vs[SSA];              // SOC slot holds a real block
     int soc_owner[SSA];        // primitive (0/1) owning the block in SOC slot b
 
     DCOL_HD bool vort(int k) const { return k * LPP + q < o; }
+    // column offset of a primitive's extra columns (static 0 unless N >= 6 can be case 4)
+    DCOL_HD int xoff(bool p2) const { return (N >= 6 && p2) ? xo2 : 0; }
+    // value of column j >= 4 of a row whose primitive puts (e0, e1) at columns 4+off, 5+off
+    DCOL_HD static double excol(int j, int off, double e0, double e1) {
+        const int t = j - 4 - off;
+        return t == 0 ? e0 : (t == 1 ? e1 : 0.0);
+    }
     DCOL_HD bool vrow(int k) const { return k < OR ? vort(k) : vs[(k - OR) / 4]; }
 
     // -------- assembly (problem_matrices.py + combine_problem_matrices.py) --------------
@@ -419,6 +429,7 @@ struct Solver {
     DCOL_HD void assemble(const KArgs& A, const DevShape& S1, const DevShape& S2, const Frame& F1, const Frame& F2) {
         o1 = S1.n_ort;
         o = o1 + S2.n_ort;
+        xo2 = (S1.n_extra > 0 && S2.n_extra > 0) ? S1.n_extra : 0;
         deg = o + NSOC;                                   // quirk Q7
         const double* __restrict__ rows = reinterpret_cast<const double*>(A.rows);
 #pragma unroll
@@ -442,8 +453,9 @@ struct Solver {
             const double u1 = Qe[3] * a0 + Qe[4] * a1 + Qe[5] * a2;
             const double u2 = Qe[6] * a0 + Qe[7] * a1 + Qe[8] * a2;
             G[k][0] = u0; G[k][1] = u1; G[k][2] = u2; G[k][3] = g3;
-            if constexpr (N > 4) G[k][4] = e0;
-            if constexpr (N > 5) G[k][5] = e1;
+            const int off = xoff(p2);
+#pragma unroll
+            for (int j = 4; j < N; ++j) G[k][j] = excol(j, off, e0, e1);
             r[k] = u0 * re[0] + u1 * re[1] + u2 * re[2];
         }
         // global SOC block 0 = first primitive with a SOC, block 1 = prim 2 when both have one
@@ -461,7 +473,7 @@ struct Solver {
             for (int c = 0; c < 3; ++c) re[c] = p2 ? F2.re[c] : F1.re[c];
             const int kind = vs[b] ? (p2 ? S2.soc_kind : S1.soc_kind) : SOC_NONE;
             soc_rows(kind, p2 ? S2.R : S1.R, p2 ? S2.cone_c : S1.cone_c, p2 ? S2.tanb : S1.tanb,
-                     p2 ? S2.n_extra : S1.n_extra, Qe, re, &G[OR + 4 * b], &r[OR + 4 * b]);
+                     p2 ? S2.n_extra : S1.n_extra, xoff(p2), Qe, re, &G[OR + 4 * b], &r[OR + 4 * b]);
         }
     }
 
@@ -469,7 +481,7 @@ struct Solver {
     // capsule/cylinder/polygon): [0 0 0 -R | 0..], h 0;  [-e_k | 0 | Qe[k][0..nx)], h -re[k]
     //   (problem_matrices.py:21-28, 66-76, 112-119, 165-176)
     // Cone: [-E Qe' | -(tanb 3H/4) e_0], h = -E Qe' re; 4th row zero  (problem_matrices.py:138-145)
-    DCOL_HD static void soc_rows(int kind, double R, double cc, double tb, int nx, const double* Qe,
+    DCOL_HD static void soc_rows(int kind, double R, double cc, double tb, int nx, int off, const double* Qe,
                                  const double* re, double (*Gb)[N], double* hb) {
         if (kind == SOC_CONE) {
 #pragma unroll
@@ -497,8 +509,9 @@ struct Solver {
 #pragma unroll
                 for (int j = 0; j < 3; ++j) Gb[k + 1][j] = (j == k) ? -1.0 : 0.0;
                 Gb[k + 1][3] = 0.0;
-                if constexpr (N > 4) Gb[k + 1][4] = (nx >= 1) ? Qe[3 * k] : 0.0;
-                if constexpr (N > 5) Gb[k + 1][5] = (nx >= 2) ? Qe[3 * k + 1] : 0.0;
+                const double c0 = (nx >= 1) ? Qe[3 * k] : 0.0, c1 = (nx >= 2) ? Qe[3 * k + 1] : 0.0;
+#pragma unroll
+                for (int j = 4; j < N; ++j) Gb[k + 1][j] = excol(j, off, c0, c1);
                 hb[k + 1] = -re[k];
             }
         } else {
@@ -971,8 +984,9 @@ struct Solver {
                 const double u1 = Fr.Qe[3] * q0.x + Fr.Qe[4] * q0.y + Fr.Qe[5] * q1.x;
                 const double u2 = Fr.Qe[6] * q0.x + Fr.Qe[7] * q0.y + Fr.Qe[8] * q1.x;
                 double gx = u0 * x[0] + u1 * x[1] + u2 * x[2] + q1.y * x[3];
-                if constexpr (N > 4) gx += q2.x * x[4];
-                if constexpr (N > 5) gx += q2.y * x[5];
+                const int off = xoff(prim == 1);
+#pragma unroll
+                for (int j = 4; j < N; ++j) gx += excol(j, off, q2.x, q2.y) * x[j];
                 const double hh = u0 * Fr.re[0] + u1 * Fr.re[1] + u2 * Fr.re[2];
                 acc += z[k] * (gx - hh);
             }
@@ -981,7 +995,7 @@ struct Solver {
         for (int b = 0; b < SS; ++b) {
             if (vs[b] && soc_owner[b] == prim) {
                 double Gb[4][N], hb[4];
-                soc_rows(S.soc_kind, S.R, S.cone_c, S.tanb, S.n_extra, Fr.Qe, Fr.re, Gb, hb);
+                soc_rows(S.soc_kind, S.R, S.cone_c, S.tanb, S.n_extra, xoff(prim == 1), Fr.Qe, Fr.re, Gb, hb);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     double gx = Gb[e][0] * x[0];
@@ -1075,8 +1089,12 @@ struct Solver {
         }
         double xi[3] = {0.0, 0.0, 0.0};
         if (S.soc_kind == SOC_BALL) {
-            if constexpr (N > 4) xi[0] = (S.n_extra >= 1) ? x[4] : 0.0;
-            if constexpr (N > 5) xi[1] = (S.n_extra >= 2) ? x[5] : 0.0;
+            const int off = xoff(prim == 1);
+#pragma unroll
+            for (int j = 4; j < N; ++j) {
+                if (S.n_extra >= 1 && j == 4 + off) xi[0] = x[j];
+                if (S.n_extra >= 2 && j == 5 + off) xi[1] = x[j];
+            }
         }
         double e[3], d[3], c1[3], c2[3];
 #pragma unroll

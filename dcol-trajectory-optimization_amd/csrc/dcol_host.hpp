@@ -130,9 +130,10 @@ struct PairClass {
     int N, nsoc, o, omax, lpp;
 };
 
-inline PairClass classify(const DevShape& a, const DevShape& b) {
+// case4: DCOL_PLAN_CASE4 extension (both primitives with extra columns: n = 4 + e1 + e2)
+inline PairClass classify(const DevShape& a, const DevShape& b, bool case4 = false) {
     PairClass c{DCOL_OK, 4, 0, 0, 0, 0};
-    if (a.n_extra > 0 && b.n_extra > 0) {   // combine_problem_matrices.py:58-67 (case 4)
+    if (a.n_extra > 0 && b.n_extra > 0 && !case4) {   // combine_problem_matrices.py:58-67 (case 4)
         c.status = DCOL_UNSUPPORTED;
         return c;
     }

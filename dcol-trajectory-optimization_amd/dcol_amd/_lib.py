@@ -17,7 +17,9 @@ POLYTOPE, SPHERE, CONE, CAPSULE, CYLINDER, POLYGON = range(6)
 # enum dcol_status
 OK, MAXITER, UNSUPPORTED, NOT_PD, NONFINITE, TOO_LARGE = range(6)
 # enum dcol_flags
-GRAD_FD, GRAD_ENVELOPE, CONTACT = 1, 2, 4
+GRAD_FD, GRAD_ENVELOPE, CONTACT, CASE4 = 1, 2, 4, 8
+# enum dcol_plan_options
+PLAN_CASE4 = 1
 SUCCESS, ERR_ARG, ERR_HIP, ERR_NOMEM = 0, -1, -2, -3
 ABI_VERSION = 1
 
@@ -45,6 +47,7 @@ SIGNATURES = {
     "dcol_pair_dims": (c_int, [c_void_p, c_int32, c_int32, POINTER(c_int32), POINTER(c_int32),
                                POINTER(c_int32), POINTER(c_int32)]),
     "dcol_plan_create": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, POINTER(c_void_p)]),
+    "dcol_plan_create_ex": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int32, POINTER(c_void_p)]),
     "dcol_plan_destroy": (c_int, [c_void_p]),
     "dcol_plan_num_launches": (c_int, [c_void_p, POINTER(c_int32)]),
     "dcol_plan_run": (c_int, [c_void_p, c_void_p, c_void_p, c_double, c_int32, c_int32, c_void_p, c_void_p,

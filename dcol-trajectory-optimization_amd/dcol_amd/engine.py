@@ -103,7 +103,9 @@ class Table:
 class Plan:
     """Owning wrapper of a dcol_plan: a fixed pairing bucketed by kernel variant."""
 
-    def __init__(self, table: Table, s1, s2):
+    def __init__(self, table: Table, s1, s2, case4: bool = False):
+        """case4=True: solve case-4 pairs (DCOL_PLAN_CASE4 extension) instead of reporting
+        UNSUPPORTED like the reference."""
         lib = _lib.load()
         self.s1 = np.ascontiguousarray(s1, dtype=np.int32)
         self.s2 = np.ascontiguousarray(s2, dtype=np.int32)
@@ -112,8 +114,9 @@ class Plan:
         self.table = table
         self.B = int(self.s1.size)
         h = ctypes.c_void_p()
-        _lib.check(lib.dcol_plan_create(table.handle, self.B, _np_ptr(self.s1), _np_ptr(self.s2), ctypes.byref(h)),
-                   "dcol_plan_create")
+        self.case4 = bool(case4)
+        _lib.check(lib.dcol_plan_create_ex(table.handle, self.B, _np_ptr(self.s1), _np_ptr(self.s2),
+                                           _lib.PLAN_CASE4 if case4 else 0, ctypes.byref(h)), "dcol_plan_create_ex")
         self.handle = h
         n = ctypes.c_int32()
         _lib.check(lib.dcol_plan_num_launches(h, ctypes.byref(n)), "dcol_plan_num_launches")
@@ -244,16 +247,16 @@ class Engine:
                 self._table = Table(self._specs, self.device)
             return self._table
 
-    def plan(self, s1, s2, cache=True) -> Plan:
+    def plan(self, s1, s2, cache=True, case4=False) -> Plan:
         s1 = np.ascontiguousarray(s1, dtype=np.int32)
         s2 = np.ascontiguousarray(s2, dtype=np.int32)
         if not cache:
-            return Plan(self.table, s1, s2)
-        key = (s1.tobytes(), s2.tobytes())
+            return Plan(self.table, s1, s2, case4)
+        key = (s1.tobytes(), s2.tobytes(), bool(case4))
         with self._lock:
             p = self._plans.get(key)
             if p is None or p.table is not self.table:
-                p = Plan(self.table, s1, s2)
+                p = Plan(self.table, s1, s2, case4)
                 self._plans[key] = p
                 if len(self._plans) > 32:
                     self._plans.popitem(last=False)
@@ -263,14 +266,15 @@ class Engine:
 
     # ---------------------------------------------------------------- solves
     def solve_host(self, s1, s2, pose1, pose2, tol=DEFAULT_TOL, max_iter=DEFAULT_MAX_ITER, grad="fd",
-                   contact=True) -> Result:
-        """Host arrays in/out: s1, s2 int [B]; pose1, pose2 float64 [B, 6] (r, p)."""
+                   contact=True, case4=False) -> Result:
+        """Host arrays in/out: s1, s2 int [B]; pose1, pose2 float64 [B, 6] (r, p).
+        case4=True: the DCOL_CASE4 extension (see Plan)."""
         s1 = np.ascontiguousarray(s1, dtype=np.int32).reshape(-1)
         s2 = np.ascontiguousarray(s2, dtype=np.int32).reshape(-1)
         B = s1.size
         p1 = np.ascontiguousarray(pose1, dtype=np.float64).reshape(B, 6)
         p2 = np.ascontiguousarray(pose2, dtype=np.float64).reshape(B, 6)
-        flags = grad_flag(grad) | (_lib.CONTACT if contact else 0)
+        flags = grad_flag(grad) | (_lib.CONTACT if contact else 0) | (_lib.CASE4 if case4 else 0)
         alpha = np.empty(B)
         cp = np.empty((B, 3)) if contact else None
         g = np.empty((B, 12)) if flags & (_lib.GRAD_FD | _lib.GRAD_ENVELOPE) else None
@@ -284,7 +288,7 @@ class Engine:
         return Result(alpha, cp, g, iters, status)
 
     def solve_objects(self, prims1, prims2, tol=DEFAULT_TOL, max_iter=DEFAULT_MAX_ITER, grad="fd",
-                      contact=True) -> Result:
+                      contact=True, case4=False) -> Result:
         """Batched form of the drop-in: two equal-length sequences of primitive objects,
         each at its current pose."""
         s1 = np.fromiter((self.register_object(o) for o in prims1), dtype=np.int32)
@@ -293,7 +297,7 @@ class Engine:
             raise ValueError("prims1 and prims2 must have equal length")
         p1 = np.array([pose_of(o) for o in prims1]).reshape(-1, 6)
         p2 = np.array([pose_of(o) for o in prims2]).reshape(-1, 6)
-        return self.solve_host(s1, s2, p1, p2, tol, max_iter, grad, contact)
+        return self.solve_host(s1, s2, p1, p2, tol, max_iter, grad, contact, case4)
 
 
 _default: Engine | None = None

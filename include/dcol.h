@@ -63,7 +63,19 @@ enum dcol_flags {
                                z'(G(theta)x - h(theta)), step sqrt(eps) (reference mode,
                                proximity_gradient.py:50-88)                               */
     DCOL_GRAD_ENVELOPE = 2, /* the same gradient in closed form (envelope theorem)       */
-    DCOL_CONTACT = 4        /* write x[0:3] (proximity.py:51-54)                          */
+    DCOL_CONTACT = 4,       /* write x[0:3] (proximity.py:51-54)                          */
+    DCOL_CASE4 = 8          /* dcol_prox_batch_host only: solve case-4 pairs (see
+                               DCOL_PLAN_CASE4) instead of reporting DCOL_UNSUPPORTED     */
+};
+
+/* dcol_plan_create_ex options. */
+enum dcol_plan_options {
+    DCOL_PLAN_CASE4 = 1 /* EXTENSION, not reference behaviour: pairs in which BOTH primitives
+                           have extra columns (capsule/cylinder/polygon x capsule/cylinder/
+                           polygon) — combine_problem_matrices.py:58-67 raises ValueError for
+                           them — are assembled with primitive 2's extra columns placed after
+                           primitive 1's (n = 4 + e1 + e2 <= 8) and solved by the same PDIP.
+                           Without the option they get DCOL_UNSUPPORTED like the reference. */
 };
 
 /* Return codes of every entry point. */
@@ -108,6 +120,9 @@ int dcol_pair_dims(const dcol_table* table, int32_t s1, int32_t s2, int32_t* m, 
  * (knot x obstacle) pairing at every iteration (systems/<name>.py inequality_constraints_x). */
 int dcol_plan_create(const dcol_table* table, int64_t B, const int32_t* shape1,
                      const int32_t* shape2, dcol_plan** out);
+/* Same with options (enum dcol_plan_options); options = 0 is dcol_plan_create.         */
+int dcol_plan_create_ex(const dcol_table* table, int64_t B, const int32_t* shape1,
+                        const int32_t* shape2, int32_t options, dcol_plan** out);
 int dcol_plan_destroy(dcol_plan* plan);
 int dcol_plan_num_launches(const dcol_plan* plan, int32_t* n);
 
