@@ -969,48 +969,79 @@ struct Solver {
         return prim == 0 ? (i < o1) : (i >= o1 && i < o);
     }
 
-    // lane part of f_k(theta_k) = sum over rows of primitive k of z_i (G_i(theta_k) x - h_i(theta_k))
-    DCOL_HD double lag_part(const KArgs& A, const DevShape& S, int prim, const Frame& Fr) const {
+    // Pose-dependent part of f_k(theta_k) = z'(G(theta_k) x - h(theta_k)) over the rows of
+    // primitive k.  Every row of every primitive is linear in (Qe, re): orthant rows
+    // z_i((Qe a_i).(x - re) + g3_i x3 + ex_i.xe) sum to (Qe w).(x - re) + const with
+    // w = sum z_i a_i; a ball SOC block adds z_1..3 . (re + Qe[:, extras] xe) + const; a cone
+    // SOC block adds -(Qe E z_0..2).(x - re) + const.  The constants are pose-independent
+    // and cancel exactly in a forward difference, so they are never formed.
+    struct LagAgg {
+        double w[3];     // sum over owned orthant rows of z_i a_i (body frame), group-summed
+        double zs[4];    // the primitive's SOC block duals (zero if none), group-summed
+        int kind;        // SOC kind of the primitive's block
+    };
+    DCOL_HD LagAgg lag_aggregate(const KArgs& A, const DevShape& S, int prim) const {
         const double* __restrict__ rows = reinterpret_cast<const double*>(A.rows);
-        double acc = 0.0;
+        LagAgg g;
+        g.w[0] = g.w[1] = g.w[2] = 0.0;
+        g.zs[0] = g.zs[1] = g.zs[2] = g.zs[3] = 0.0;
+        g.kind = S.soc_kind;
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
             if (owns_row(k, prim)) {
                 const int i = k * LPP + q;
                 const int ri = S.row_off + ((prim == 0) ? i : (i - o1));
                 const double2* rw = reinterpret_cast<const double2*>(rows + 8 * (int64_t)ri);
-                const double2 q0 = rw[0], q1 = rw[1], q2 = rw[2];
-                const double u0 = Fr.Qe[0] * q0.x + Fr.Qe[1] * q0.y + Fr.Qe[2] * q1.x;
-                const double u1 = Fr.Qe[3] * q0.x + Fr.Qe[4] * q0.y + Fr.Qe[5] * q1.x;
-                const double u2 = Fr.Qe[6] * q0.x + Fr.Qe[7] * q0.y + Fr.Qe[8] * q1.x;
-                double gx = u0 * x[0] + u1 * x[1] + u2 * x[2] + q1.y * x[3];
-                const int off = xoff(prim == 1);
-#pragma unroll
-                for (int j = 4; j < N; ++j) gx += excol(j, off, q2.x, q2.y) * x[j];
-                const double hh = u0 * Fr.re[0] + u1 * Fr.re[1] + u2 * Fr.re[2];
-                acc += z[k] * (gx - hh);
+                const double2 q0 = rw[0], q1 = rw[1];
+                g.w[0] += z[k] * q0.x;
+                g.w[1] += z[k] * q0.y;
+                g.w[2] += z[k] * q1.x;
             }
         }
 #pragma unroll
-        for (int b = 0; b < SS; ++b) {
-            if (vs[b] && soc_owner[b] == prim) {
-                double Gb[4][N], hb[4];
-                soc_rows(S.soc_kind, S.R, S.cone_c, S.tanb, S.n_extra, xoff(prim == 1), Fr.Qe, Fr.re, Gb, hb);
+        for (int b = 0; b < SS; ++b)
+            if (vs[b] && soc_owner[b] == prim)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    double gx = Gb[e][0] * x[0];
+                for (int e = 0; e < 4; ++e) g.zs[e] = z[OR + 4 * b + e];
 #pragma unroll
-                    for (int j = 1; j < N; ++j) gx += Gb[e][j] * x[j];
-                    acc += z[OR + 4 * b + e] * (gx - hb[e]);
-                }
-            }
+        for (int c = 0; c < 3; ++c) g.w[c] = R::sum(g.w[c]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) g.zs[e] = R::sum(g.zs[e]);
+        return g;
+    }
+    DCOL_HD double lag_pose_part(const LagAgg& g, const DevShape& S, int prim, const Frame& Fr) const {
+        double d[3], v[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            d[c] = x[c] - Fr.re[c];
+            v[c] = g.w[c];
         }
-        return acc;
+        if (g.kind == SOC_CONE) {          // a_k = -E_kk e_k for the three cone rows
+            v[0] -= S.tanb * g.zs[0];
+            v[1] -= g.zs[1];
+            v[2] -= g.zs[2];
+        }
+        double f = 0.0;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) f += (Fr.Qe[3 * r] * v[0] + Fr.Qe[3 * r + 1] * v[1] + Fr.Qe[3 * r + 2] * v[2]) * d[r];
+        if (g.kind == SOC_BALL) {
+            const int off = xoff(prim == 1);
+            double xe0 = 0.0, xe1 = 0.0;
+#pragma unroll
+            for (int j = 4; j < N; ++j) {
+                if (S.n_extra >= 1 && j == 4 + off) xe0 = x[j];
+                if (S.n_extra >= 2 && j == 5 + off) xe1 = x[j];
+            }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) f += g.zs[k + 1] * (Fr.re[k] + Fr.Qe[3 * k] * xe0 + Fr.Qe[3 * k + 1] * xe1);
+        }
+        return f;
     }
 
-    // scipy approx_fprime(theta, f, sqrt(eps)) restricted to primitive prim's 6 coordinates.
-    // Translation perturbations keep the rotation: only r_eff = r + Q r_offset moves; the
-    // three rotation perturbations are evaluated together (independent chains, ILP).
+    // scipy approx_fprime(theta, f, sqrt(eps)) restricted to primitive prim's 6 coordinates
+    // (proximity_gradient.py:50-88): forward differences of f_k with the reference's step
+    // rule, f_k evaluated through lag_aggregate / lag_pose_part.  Translation perturbations
+    // keep the rotation (only r_eff moves).
     DCOL_HD void fd_grad_prim(const KArgs& A, const DevShape& S, int prim, const double th0[6], double* g) const {
         const double hstep = 1.4901161193847656e-08;   // sqrt(finfo(float).eps)
         double tj[6], dxj[6];
@@ -1022,16 +1053,16 @@ struct Solver {
             tj[j] = th0[j] + hj;
             dxj[j] = tj[j] - th0[j];
         }
+        const LagAgg ag = lag_aggregate(A, S, prim);
         Frame F0;
         make_frame(S, th0, F0);
-        double f[7];
-        f[0] = lag_part(A, S, prim, F0);
+        const double f0 = lag_pose_part(ag, S, prim, F0);
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
             Frame Fj = F0;
 #pragma unroll
             for (int c = 0; c < 3; ++c) Fj.re[c] = (c == j ? tj[j] : th0[c]) + F0.qro[c];
-            f[1 + j] = lag_part(A, S, prim, Fj);
+            g[j] = (lag_pose_part(ag, S, prim, Fj) - f0) / dxj[j];
         }
 #pragma unroll
         for (int j = 3; j < 6; ++j) {
@@ -1040,12 +1071,8 @@ struct Solver {
             for (int c = 0; c < 6; ++c) th[c] = (c == j) ? tj[j] : th0[c];
             Frame Fj;
             make_frame(S, th, Fj);
-            f[1 + j] = lag_part(A, S, prim, Fj);
+            g[j] = (lag_pose_part(ag, S, prim, Fj) - f0) / dxj[j];
         }
-#pragma unroll
-        for (int j = 0; j < 7; ++j) f[j] = R::sum(f[j]);
-#pragma unroll
-        for (int j = 0; j < 6; ++j) g[j] = (f[1 + j] - f[0]) / dxj[j];
     }
 
     // closed-form d/dtheta_k of z'(G(theta)x - h(theta)) (see DESIGN.md "gradient modes"):
@@ -1223,6 +1250,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
 #define DCOL_BLOCK 64
 #endif
 constexpr int kSolveBlock = DCOL_BLOCK;
+static_assert(kSolveBlock % 64 == 0, "one or more whole waves per workgroup");
 
 template <int N, int NSOC, int OMAX, int LPP, int WPS>
 __global__ void __launch_bounds__(kSolveBlock, WPS) prox_kernel(KArgs A) {
