@@ -48,8 +48,15 @@ victim_poses = _common.rigid_victim_poses
 state_jacobian = _common.rigid_state_jacobian
 
 
-def obstacles():
-    d = _data.load()
+def obstacles(jld2_path=None):
+    """The reference's eleven obstacles; the 8-face polytope comes from polytopes.jld2
+    (read with altro.systems.jld2 when a path is given, else the decoded copy shipped in
+    altro/data)."""
+    if jld2_path is not None:
+        from . import jld2
+        d = {f"jld2_{k}": v for k, v in jld2.read(jld2_path, ["A2", "b2"]).items()}
+    else:
+        d = _data.load()
     poly = create_n_sided(5, 0.6)
     floor = create_rect_prism(length=20, width=5, height=0.2)
     floor.r = [0, 0, 0.9]
@@ -64,12 +71,12 @@ def obstacles():
     return obs
 
 
-def initialize():
+def initialize(jld2_path=None):
     """-> (params, X, U) of the quadrotor problem."""
     nx, nu, N, dt = 12, 4, 100, 0.08
     x0 = np.array([-8, 0, 4, 0, 0, 0.0, 0, 0, 0, 0, 0, 0])
     xg = np.array([8, 0, 4, 0, 0, 0.0, 0, 0, 0, 0, 0, 0])
-    P_obs = obstacles()
+    P_obs = obstacles(jld2_path)
     params = dict(nx=nx, nu=nu, ncx=len(P_obs), ncu=2 * nu, N=N, Q=np.diag(np.ones(nx)), R=np.diag(np.ones(nu)),
                   Qf=np.diag(np.ones(nx)), u_min=-2000 * np.ones(nu), u_max=2000 * np.ones(nu),
                   Xref=_common.linear_interp(dt, x0, xg, N), Uref=[(9.81 * 0.5 / 4) * np.ones(nu) for _ in range(N)],
