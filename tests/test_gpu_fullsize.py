@@ -1,0 +1,131 @@
+"""Full-size checks on the benchmark workload (BASELINE.json configs[3]: 100k random
+polytope-polytope pairs; and 1M) through size-independent properties of the problem,
+plus an exact comparison with the C oracle on a sample of the same batch.
+
+Properties (exact for the mathematical problem; tolerances cover pdip_tol = 1e-6 and the
+FD step):
+  * every pair converges, alpha > 0 and finite, iters <= 50;
+  * swap symmetry: alpha(A, B) = alpha(B, A) and the gradient halves swap;
+  * translation invariance: shifting both poses by t leaves alpha unchanged and
+    d alpha / d r1 + d alpha / d r2 = 0;
+  * the contact point lies in both primitives scaled by alpha (up to the exit residual);
+  * FD and envelope gradients agree; chunked launches equal one launch bitwise.
+"""
+import numpy as np
+import pytest
+
+from conftest import alpha_close, grad_close, gpu_available
+
+pytestmark = pytest.mark.gpu
+
+B = 100_000
+
+
+@pytest.fixture(scope="module")
+def batch():
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import bench
+    from dcol_amd import Engine, spec_from_arrays
+    tab = bench.shape_table()
+    s1, s2, p1, p2 = bench.pairs(B, len(tab["type"]), seed=1000)
+    eng = Engine(device=0)
+    ids = np.array([eng.register(spec_from_arrays(tab, k)) for k in range(len(tab["type"]))], np.int32)
+    res = eng.solve_host(ids[s1], ids[s2], p1, p2, grad="fd")
+    return dict(tab=tab, s1=s1, s2=s2, p1=p1, p2=p2, eng=eng, ids=ids, res=res)
+
+
+def test_all_converge(batch):
+    r = batch["res"]
+    assert (r.status == 0).all()
+    assert (r.iters <= 50).all() and (r.iters > 0).all()
+    assert np.isfinite(r.alpha).all() and (r.alpha > 0).all()
+    assert np.isfinite(r.grad).all()
+
+
+def test_sample_matches_c_oracle(batch):
+    from oracle import c_oracle
+    n = 4000
+    ref = c_oracle.run_batch(batch["tab"], batch["s1"][:n], batch["s2"][:n], batch["p1"][:n], batch["p2"][:n],
+                             want_grad=True, threads=16)
+    r = batch["res"]
+    assert np.array_equal(r.status[:n], ref["status"])
+    assert np.mean(r.iters[:n] == ref["iters"]) >= 0.999
+    assert alpha_close(r.alpha[:n], ref["alpha"]).all()
+    assert grad_close(r.grad[:n], ref["grad"]).all()
+
+
+def test_swap_symmetry(batch):
+    b, ids = batch, batch["ids"]
+    sw = b["eng"].solve_host(ids[b["s2"]], ids[b["s1"]], b["p2"], b["p1"], grad="fd")
+    r = b["res"]
+    assert (sw.status == 0).all()
+    np.testing.assert_allclose(sw.alpha, r.alpha, rtol=2e-5, atol=1e-9)
+    g_sw = np.concatenate([sw.grad[:, 6:], sw.grad[:, :6]], axis=1)
+    scale = np.maximum(np.abs(r.grad).max(axis=1), 1.0)
+    assert (np.abs(g_sw - r.grad).max(axis=1) <= 1e-3 * scale).all()
+
+
+def test_translation_invariance(batch):
+    b, ids = batch, batch["ids"]
+    t = np.array([0.7, -1.3, 2.1])
+    q1, q2 = b["p1"].copy(), b["p2"].copy()
+    q1[:, :3] += t
+    q2[:, :3] += t
+    sh = b["eng"].solve_host(ids[b["s1"]], ids[b["s2"]], q1, q2, grad="envelope")
+    r = b["res"]
+    np.testing.assert_allclose(sh.alpha, r.alpha, rtol=1e-6, atol=1e-12)
+    scale = np.maximum(np.abs(sh.grad).max(axis=1), 1.0)
+    assert (np.abs(sh.grad[:, 0:3] + sh.grad[:, 6:9]).max(axis=1) <= 1e-6 * scale).all()
+
+
+def test_contact_point_in_both_scaled_prisms(batch):
+    from oracle.dcol_oracle import dcm_from_mrp
+    b, r = batch, batch["res"]
+    tab = b["tab"]
+    half = tab["b_pool"].reshape(-1, 6)[:, :3]            # rect prism half-dims
+    idx = np.arange(0, B, 97)
+    for i in idx:
+        a = r.alpha[i]
+        c = r.contact[i]
+        for s, p in ((b["s1"][i], b["p1"][i]), (b["s2"][i], b["p2"][i])):
+            y = dcm_from_mrp(p[3:]).T @ (c - p[:3])
+            # the PDIP stops on mu alone (pdip.py:416-422), so the primal residual G x + s - h
+            # at exit is small but not zero (~1e-5 relative here, same as the reference)
+            assert (np.abs(y) <= a * half[s] * (1 + 1e-4) + 1e-9).all(), i
+
+
+def test_fd_matches_envelope(batch):
+    b, ids = batch, batch["ids"]
+    env = b["eng"].solve_host(ids[b["s1"]], ids[b["s2"]], b["p1"], b["p2"], grad="envelope")
+    assert np.array_equal(env.alpha, b["res"].alpha)          # same solve, bitwise
+    assert grad_close(env.grad, b["res"].grad).all()
+
+
+def test_chunked_equals_single_launch_1m():
+    """1M pairs (the large configuration): one launch vs ten 100k launches, bitwise."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import torch
+
+    import bench
+    from dcol_amd import Engine, alloc_outputs, spec_from_arrays
+    tab = bench.shape_table()
+    n = 1_000_000
+    s1, s2, p1, p2 = bench.pairs(n, len(tab["type"]), seed=7)
+    eng = Engine(device=0)
+    ids = np.array([eng.register(spec_from_arrays(tab, k)) for k in range(len(tab["type"]))], np.int32)
+    dev = torch.device("cuda", 0)
+    d1 = torch.from_numpy(np.ascontiguousarray(p1.T)).to(dev)
+    d2 = torch.from_numpy(np.ascontiguousarray(p2.T)).to(dev)
+    whole = eng.plan(ids[s1], ids[s2], cache=False).run(d1, d2, grad="fd", contact=False)
+    alpha = whole["alpha"].cpu().numpy()
+    status = whole["status"].cpu().numpy()
+    assert (status == 0).all()
+    c = 100_000
+    for k in range(0, n, c):
+        out = alloc_outputs(c, dev, want_grad=True, want_contact=False)
+        plan = eng.plan(ids[s1[k:k + c]], ids[s2[k:k + c]], cache=False)
+        part = plan.run(d1[:, k:k + c].contiguous(), d2[:, k:k + c].contiguous(), grad="fd", contact=False, out=out)
+        assert np.array_equal(part["alpha"].cpu().numpy(), alpha[k:k + c])
+        assert torch.equal(part["grad"], whole["grad"][:, k:k + c])
