@@ -122,7 +122,7 @@ struct KArgs {
     int32_t* __restrict__ iters;        // [B]
     int32_t* __restrict__ status;       // [B]
 #ifdef DCOL_STAMPS
-    unsigned long long* stamps;         // diagnostic build only (tools/stamp_probe.hip): [B][8]
+    unsigned long long* stamps;         // diagnostic build only (tools/stamp_probe.hip): [B][16]
 #endif
 };
 
@@ -133,11 +133,25 @@ struct KArgs {
         unsigned long long t_;                                                          \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");      \
         __builtin_amdgcn_sched_barrier(0);                                              \
-        if ((q) == 0) (A).stamps[8 * (pi) + (k)] = t_;                                  \
+        if ((q) == 0) (A).stamps[16 * (pi) + (k)] = t_;                                 \
+    } while (0)
+// sub-phases of PDIP iteration 2 into stamps[16 * pi + 8 + k] (Solver::dbg)
+#define DCOL_ISTAMP(it, k)                                                              \
+    do {                                                                                \
+        if ((it) == 2 && dbg) {                                                         \
+            __builtin_amdgcn_sched_barrier(0);                                          \
+            unsigned long long t_;                                                      \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");  \
+            __builtin_amdgcn_sched_barrier(0);                                          \
+            dbg[k] = t_;                                                                \
+        }                                                                               \
     } while (0)
 #else
 #define DCOL_STAMP(A, pi, q, k) \
     do {                        \
+    } while (0)
+#define DCOL_ISTAMP(it, k) \
+    do {                   \
     } while (0)
 #endif
 
@@ -412,6 +426,9 @@ struct Solver {
                                // case-4 pair (both primitives have extras; opt-in extension),
                                // else 0 (combine_problem_matrices.py cases 1-3)
     bool vs[SSA];              // SOC slot holds a real block
+#ifdef DCOL_STAMPS
+    unsigned long long* dbg = nullptr;
+#endif
     int soc_owner[SSA];        // primitive (0/1) owning the block in SOC slot b
 
     DCOL_HD bool vort(int k) const { return k * LPP + q < o; }
@@ -671,11 +688,13 @@ struct Solver {
     }
 
     // line-search candidate: keep argmin of x / (-d) over d < 0 by cross-multiplication
-    DCOL_HD static void ratio(double xv, double d, double& bn, double& bd) {
-        if (d < 0.0) {
-            const double nd = -d;
-            if (xv * bd < bn * nd) { bn = xv; bd = nd; }
-        }
+    // Branch-free (selects, no exec-mask branches): the hot loop runs one of these per
+    // row bound per direction, and a divergent branch costs more than the compare.
+    DCOL_HD static void ratio(double xv, double d, bool valid, double& bn, double& bd) {
+        const double nd = -d;
+        const bool take = valid & (d < 0.0) & (xv * bd < bn * nd);
+        bn = take ? xv : bn;
+        bd = take ? nd : bd;
     }
 
     struct SocState {
@@ -689,6 +708,7 @@ struct Solver {
         int it = 0;
         int32_t st = ST_MAXITER;
         for (it = 0; it < max_iter; ++it) {
+            DCOL_ISTAMP(it, 0);
             // ---- NT scalings, residuals, normal matrix (pdip.py:410-434)
             double il[OR > 0 ? OR : 1];
             SocState so[SSA];
@@ -703,7 +723,7 @@ struct Solver {
             for (int k = 0; k < OR; ++k) {
                 const double sk = s[k], zk = z[k];
                 il[k] = frsqrt(sk * zk);                  // 1/lambda, lambda = sqrt(s z)
-                if (vort(k)) sz += sk * zk;
+                sz = fma(vort(k) ? sk : 0.0, zk, sz);
                 const double wi = zk * il[k];
                 double g[N];
 #pragma unroll
@@ -753,6 +773,7 @@ struct Solver {
             allsum_vec(rx);
             allsum_sym(Hm);
             rx[3] += 1.0;                                   // + c (c = e_3)
+            DCOL_ISTAMP(it, 1);
             const double mu = sz / (double)deg;
             if (mu < tol) {                                 // quirk Q3
                 st = ST_OK;
@@ -766,6 +787,7 @@ struct Solver {
             if (!finite) { st = ST_NONFINITE; break; }       // scipy check_finite -> ValueError
             double F[N][N], idg[N];
             if (!chol(Hm, F, idg)) { st = ST_NOT_PD; break; }
+            DCOL_ISTAMP(it, 2);
 
             // ---- predictor (affine) direction
             double dsA[M], dzA[M];
@@ -774,10 +796,11 @@ struct Solver {
             double bn = 1.0, bd = 1.0, als = 1.0;
             step_bound(so, dsA, dzA, bn, bd, als);
             const double aa = R::min(fmin(bn / bd, als));           // quirk Q5 (no 0.99)
+            DCOL_ISTAMP(it, 3);
             double rho = 0.0;
 #pragma unroll
             for (int k = 0; k < M; ++k)
-                if (vrow(k)) rho += (s[k] + aa * dsA[k]) * (z[k] + aa * dzA[k]);
+                rho = fma(vrow(k) ? s[k] + aa * dsA[k] : 0.0, z[k] + aa * dzA[k], rho);
             rho = R::sum(rho) * frcp(sz);
             const double sc = fmax(0.0, fmin(1.0, rho));
             const double sigma = sc * sc * sc;                      // quirk Q6
@@ -798,16 +821,16 @@ struct Solver {
             // test as they are produced and recomputed in the update (register budget).
             const double smu = sigma * mu;
             double sbzt[SSA][4], slds[SSA][4];
+            DCOL_ISTAMP(it, 4);
             rhs_solve(so, il, F, idg, rx, cp, smu, dx, sbzt, slds);
+            DCOL_ISTAMP(it, 5);
             bn = 1.0; bd = 1.0; als = 1.0;
 #pragma unroll
             for (int k = 0; k < OR; ++k) {
                 double u, dzk, dsk;
                 orth_step(k, il, cp, smu, dx, u, dzk, dsk);
-                if (vort(k)) {
-                    ratio(s[k], dsk, bn, bd);
-                    ratio(z[k], dzk, bn, bd);
-                }
+                ratio(s[k], dsk, vort(k), bn, bd);
+                ratio(z[k], dzk, vort(k), bn, bd);
             }
             double sdz[SSA][4], sds[SSA][4], su[SSA][4];
 #pragma unroll
@@ -819,6 +842,7 @@ struct Solver {
                 }
             }
             const double a = fmin(1.0, 0.99 * R::min(fmin(bn / bd, als)));
+            DCOL_ISTAMP(it, 6);
 #pragma unroll
             for (int j = 0; j < N; ++j) x[j] += a * dx[j];
 #pragma unroll
@@ -826,10 +850,9 @@ struct Solver {
                 double u, dzk, dsk;
                 orth_step(k, il, cp, smu, dx, u, dzk, dsk);
                 r[k] += a * u;
-                if (vort(k)) {
-                    s[k] += a * dsk;
-                    z[k] += a * dzk;
-                }
+                const bool v = vort(k);
+                s[k] = v ? s[k] + a * dsk : s[k];
+                z[k] = v ? z[k] + a * dzk : z[k];
             }
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
@@ -843,6 +866,7 @@ struct Solver {
                     }
                 }
             }
+            DCOL_ISTAMP(it, 7);
         }
         *it_out = it;
         return st;
@@ -948,10 +972,8 @@ struct Solver {
                             double& als) const {
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
-            if (vort(k)) {
-                ratio(s[k], ds[k], bn, bd);
-                ratio(z[k], dz[k], bn, bd);
-            }
+            ratio(s[k], ds[k], vort(k), bn, bd);
+            ratio(z[k], dz[k], vort(k), bn, bd);
         }
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
@@ -1184,6 +1206,9 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
 
     Solver<N, NSOC, OMAX, LPP> P;
     P.q = q;
+#ifdef DCOL_STAMPS
+    P.dbg = (q == 0) ? A.stamps + 16 * pi + 8 : nullptr;
+#endif
     P.assemble(A, S1, S2, F1, F2);
     DCOL_STAMP(A, pi, q, 2);
     int it = 0;

@@ -79,14 +79,14 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dp2, 48 * B));
     CK(hipMalloc(&dal, 8 * B));
     CK(hipMalloc(&dgr, 96 * B));
-    CK(hipMalloc(&dstamp, 64 * B));
+    CK(hipMalloc(&dstamp, 128 * B));
     CK(hipMemcpy(dsh, sh.data(), sizeof(DevShape) * NS, hipMemcpyHostToDevice));
     CK(hipMemcpy(drw, rows.data(), sizeof(DevRow) * rows.size(), hipMemcpyHostToDevice));
     CK(hipMemcpy(ds1, s1.data(), 4 * B, hipMemcpyHostToDevice));
     CK(hipMemcpy(ds2, s2.data(), 4 * B, hipMemcpyHostToDevice));
     CK(hipMemcpy(dp1, p1.data(), 48 * B, hipMemcpyHostToDevice));
     CK(hipMemcpy(dp2, p2.data(), 48 * B, hipMemcpyHostToDevice));
-    CK(hipMemset(dstamp, 0, 64 * B));
+    CK(hipMemset(dstamp, 0, 128 * B));
     KArgs a;
     std::memset(&a, 0, sizeof(a));
     a.shapes = dsh; a.rows = drw; a.s1 = ds1; a.s2 = ds2; a.pose1 = dp1; a.pose2 = dp2; a.perm = nullptr;
@@ -98,9 +98,9 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL((prox_kernel<4, 0, 12, LPP, 2>), dim3(grid), dim3(kSolveBlock), 0, 0, a);
         CK(hipDeviceSynchronize());
     }
-    std::vector<unsigned long long> st(8 * B);
+    std::vector<unsigned long long> st(16 * B);
     std::vector<int32_t> it(B), stat(B);
-    CK(hipMemcpy(st.data(), dstamp, 64 * B, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(st.data(), dstamp, 128 * B, hipMemcpyDeviceToHost));
     CK(hipMemcpy(it.data(), dit, 4 * B, hipMemcpyDeviceToHost));
     CK(hipMemcpy(stat.data(), dst, 4 * B, hipMemcpyDeviceToHost));
     const char* names[5] = {"loads+frames", "assembly", "initialize", "pdip loop", "gradient"};
@@ -109,16 +109,16 @@ int main(int argc, char** argv) {
     double it_mean = 0, it_wmax = 0;
     unsigned long long t_first = ~0ull, t_last = 0;
     for (int64_t i = 0; i < B; ++i) {
-        for (int k = 0; k < 5; ++k) sum[k] += (double)(st[8 * i + k + 1] - st[8 * i + k]);
+        for (int k = 0; k < 5; ++k) sum[k] += (double)(st[16 * i + k + 1] - st[16 * i + k]);
         it_mean += it[i];
-        t_first = std::min(t_first, st[8 * i]);
-        t_last = std::max(t_last, st[8 * i + 5]);
+        t_first = std::min(t_first, st[16 * i]);
+        t_last = std::max(t_last, st[16 * i + 5]);
     }
     for (int64_t w = 0; w * PW < B; ++w) {
         double m[5] = {0};
         int im = 0;
         for (int64_t i = w * PW; i < std::min<int64_t>(B, (w + 1) * PW); ++i) {
-            for (int k = 0; k < 5; ++k) m[k] = std::max(m[k], (double)(st[8 * i + k + 1] - st[8 * i + k]));
+            for (int k = 0; k < 5; ++k) m[k] = std::max(m[k], (double)(st[16 * i + k + 1] - st[16 * i + k]));
             im = std::max(im, it[i]);
         }
         for (int k = 0; k < 5; ++k) wmax[k] += m[k];
@@ -129,6 +129,18 @@ int main(int argc, char** argv) {
                 it_wmax / nw);
     for (int k = 0; k < 5; ++k)
         std::printf("  %-14s mean %9.0f cyc/pair   per-wave max %9.0f cyc\n", names[k], sum[k] / B, wmax[k] / nw);
-    std::printf("  span first->last stamp: %.0f cyc\n", (double)(t_last - t_first));
+    // sub-phases of PDIP iteration 2 (pairs that reached it)
+    const char* sub[7] = {"NT + normal matrix", "Cholesky", "predictor + bound", "rho, sigma, cp",
+                          "corrector rhs", "corrector bound", "update"};
+    double ss[7] = {0};
+    int64_t cnt = 0;
+    for (int64_t i = 0; i < B; ++i) {
+        const unsigned long long* t = &st[16 * i + 8];
+        if (t[0] == 0 || t[7] == 0) continue;
+        ++cnt;
+        for (int k = 0; k < 7; ++k) ss[k] += (double)(t[k + 1] - t[k]);
+    }
+    std::printf("  iteration 2 (%lld pairs):\n", (long long)cnt);
+    for (int k = 0; k < 7; ++k) std::printf("    %-20s %8.0f cyc\n", sub[k], cnt ? ss[k] / cnt : 0.0);
     return 0;
 }
