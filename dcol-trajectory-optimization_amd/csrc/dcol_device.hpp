@@ -604,18 +604,15 @@ struct Solver {
         double any = 0.0, mn = __builtin_inf(), socv = -__builtin_inf();
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
-            if (vort(k)) {
-                if (v[k] <= 0.0) any = 1.0;
-                mn = fmin(mn, v[k]);
-            }
+            const bool vk = vort(k);
+            any = (vk & (v[k] <= 0.0)) ? 1.0 : any;
+            mn = vk ? fmin(mn, v[k]) : mn;
         }
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
-            if (vs[b]) {
-                const double* p = v + OR + 4 * b;
-                const double res = p[0] - sqrt(p[1] * p[1] + p[2] * p[2] + p[3] * p[3]);
-                if (res <= 0.0) socv = fmax(socv, -res);
-            }
+            const double* p = v + OR + 4 * b;
+            const double res = p[0] - sqrt(p[1] * p[1] + p[2] * p[2] + p[3] * p[3]);
+            socv = (vs[b] & (res <= 0.0)) ? fmax(socv, -res) : socv;
         }
         any = R::max(any);
         mn = R::min(mn);
@@ -626,11 +623,9 @@ struct Solver {
         if (a >= 0.0) {
             const double sh = 1.0 + a;
 #pragma unroll
-            for (int k = 0; k < OR; ++k)
-                if (vort(k)) v[k] += sh;
+            for (int k = 0; k < OR; ++k) v[k] = vort(k) ? v[k] + sh : v[k];
 #pragma unroll
-            for (int b = 0; b < SS; ++b)
-                if (vs[b]) v[OR + 4 * b] += sh;
+            for (int b = 0; b < SS; ++b) v[OR + 4 * b] = vs[b] ? v[OR + 4 * b] + sh : v[OR + 4 * b];
         }
     }
 
@@ -742,7 +737,8 @@ struct Solver {
                 soc_nt(s + k0, z + k0, so[b].W);
                 soc_mul(so[b].W, z + k0, so[b].lam);
                 soc_prod(so[b].lam, so[b].lam, so[b].ll);
-                if (vs[b]) sz += s[k0] * z[k0] + s[k0 + 1] * z[k0 + 1] + s[k0 + 2] * z[k0 + 2] + s[k0 + 3] * z[k0 + 3];
+                const double szb = s[k0] * z[k0] + s[k0 + 1] * z[k0 + 1] + s[k0 + 2] * z[k0 + 2] + s[k0 + 3] * z[k0 + 3];
+                sz = vs[b] ? sz + szb : sz;
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -836,10 +832,9 @@ struct Solver {
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
                 soc_step(so[b], OR + 4 * b, sbzt[b], slds[b], dx, su[b], sdz[b], sds[b]);
-                if (vs[b]) {
-                    const int k0 = OR + 4 * b;
-                    als = fmin(als, fmin(soc_ls(s + k0, sds[b]), soc_ls(z + k0, sdz[b])));
-                }
+                const int k0 = OR + 4 * b;
+                const double lb = fmin(soc_ls(s + k0, sds[b]), soc_ls(z + k0, sdz[b]));
+                als = vs[b] ? fmin(als, lb) : als;
             }
             const double a = fmin(1.0, 0.99 * R::min(fmin(bn / bd, als)));
             DCOL_ISTAMP(it, 6);
@@ -860,10 +855,8 @@ struct Solver {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     r[k0 + e] += a * su[b][e];
-                    if (vs[b]) {
-                        s[k0 + e] += a * sds[b][e];
-                        z[k0 + e] += a * sdz[b][e];
-                    }
+                    s[k0 + e] = vs[b] ? s[k0 + e] + a * sds[b][e] : s[k0 + e];
+                    z[k0 + e] = vs[b] ? z[k0 + e] + a * sdz[b][e] : z[k0 + e];
                 }
             }
             DCOL_ISTAMP(it, 7);
@@ -977,10 +970,9 @@ struct Solver {
         }
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
-            if (vs[b]) {
-                const int k0 = OR + 4 * b;
-                als = fmin(als, fmin(soc_ls(s + k0, ds + k0), soc_ls(z + k0, dz + k0)));
-            }
+            const int k0 = OR + 4 * b;
+            const double lb = fmin(soc_ls(s + k0, ds + k0), soc_ls(z + k0, dz + k0));
+            als = vs[b] ? fmin(als, lb) : als;
         }
         (void)so;
     }
