@@ -109,7 +109,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check", type=int, default=256, help="pairs re-checked against the oracle")
     ap.add_argument("--max-iter", type=int, default=50, help="PDIP iteration cap (diagnostics only; reference: 50)")
-    ap.add_argument("--no-altro", action="store_true", help="skip the ALTRO wall-clock section")
+    ap.add_argument("--no-altro", action="store_true", help="skip the ALTRO wall-clock and scene-batch sections")
+    ap.add_argument("--workload", choices=["poly100k", "mixed1m"], default="poly100k",
+                    help="poly100k: BASELINE configs[3], 100k poly-poly pairs per GPU (weak scaling, the "
+                         "headline); mixed1m: configs[4], 1M mixed pairs sharded over the GPUs + one "
+                         "all-gather (strong scaling)")
     ap.add_argument("--backend", default=os.environ.get("DCOL_DIST_BACKEND", "nccl"),
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo for rehearsals)")
     args = ap.parse_args()
@@ -132,6 +136,8 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local)
     coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
+    if args.workload == "mixed1m":
+        return run_mixed(args, world, rank, local, dev, coll_dev, dist)
 
     from dcol_amd import Engine, spec_from_arrays
     tab = shape_table()
@@ -234,12 +240,190 @@ def main():
                                 "alpha_ok": bool(a_ok), "grad_ok": bool(g_ok)}
     if world == 1 and not args.no_altro:
         line["altro"] = altro_section()
+        line["scene_batches"] = scene_batches(local)
     if world == 1 and not args.no_cpu:
         workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
         line["cpu_baseline"] = cpu_baseline(tab, s1, s2, p1, p2, args.cpu_sample, workers)
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+MIXED_KINDS = (0, 1, 2, 3, 4, 5)      # polytope sphere cone capsule cylinder polygon
+
+
+def mixed_table(per_kind=64, seed=0):
+    """BASELINE configs[4] shapes: per kind `per_kind` shapes —
+    rect prisms U(0.2, 2)^3, spheres R ~ U(.2, 1), cones H ~ U(.5, 2), beta ~ U(10, 40) deg,
+    capsules / cylinders R ~ U(.1, .6), L ~ U(.3, 2), pentagons d = 0.6 with R = 0.2."""
+    rng = np.random.default_rng(seed)
+    t, nh, off, prm, A_rows, b_rows = [], [], [], [], [], []
+    ang = np.linspace(0, 2 * np.pi, 5, endpoint=False)
+    pent = np.stack([np.cos(ang), np.sin(ang)], 1)
+    box = np.array([[1.0, 0, 0], [0, 1, 0], [0, 0, 1], [-1, 0, 0], [0, -1, 0], [0, 0, -1]])
+    for kind in MIXED_KINDS:
+        for _ in range(per_kind):
+            t.append(kind)
+            off.append(len(b_rows))
+            if kind == 0:
+                d = rng.uniform(0.2, 2.0, 3)
+                A_rows += list(box)
+                b_rows += list(np.concatenate([d / 2, d / 2]))
+                nh.append(6)
+                prm.append((0, 0, 0, 0))
+            elif kind == 5:
+                A_rows += [list(a) + [0.0] for a in pent]
+                b_rows += [0.6] * 5
+                nh.append(5)
+                prm.append((0.2, 0, 0, 0))
+            else:
+                nh.append(0)
+                if kind == 1:
+                    prm.append((rng.uniform(0.2, 1.0), 0, 0, 0))
+                elif kind == 2:
+                    prm.append((0, 0, rng.uniform(0.5, 2.0), np.deg2rad(rng.uniform(10, 40))))
+                else:
+                    prm.append((rng.uniform(0.1, 0.6), rng.uniform(0.3, 2.0), 0, 0))
+    S = len(t)
+    return {"type": np.array(t, np.int32), "nh": np.array(nh, np.int32), "A_off": np.array(off, np.int32),
+            "A_pool": np.array(A_rows, dtype=np.float64).reshape(-1, 3), "b_pool": np.array(b_rows, dtype=np.float64),
+            "params": np.array(prm, dtype=np.float64), "r_offset": np.zeros((S, 3)),
+            "Q_offset": np.tile(np.eye(3), (S, 1, 1))}
+
+
+def mixed_pairs(tab, B, seed):
+    """Ordered kind pairs uniform over the 27 the reference supports (at least one of
+    polytope / sphere / cone), shapes uniform within a kind; poses as configs[3]."""
+    rng = np.random.default_rng(seed)
+    combos = [(a, b) for a in MIXED_KINDS for b in MIXED_KINDS if a <= 2 or b <= 2]
+    by_kind = {k: np.flatnonzero(tab["type"] == k) for k in MIXED_KINDS}
+    c = rng.integers(0, len(combos), B)
+    ka = np.array([combos[i][0] for i in range(len(combos))])[c]
+    kb = np.array([combos[i][1] for i in range(len(combos))])[c]
+    s1 = np.empty(B, np.int32)
+    s2 = np.empty(B, np.int32)
+    for k in MIXED_KINDS:
+        m1, m2 = ka == k, kb == k
+        s1[m1] = rng.choice(by_kind[k], m1.sum())
+        s2[m2] = rng.choice(by_kind[k], m2.sum())
+    pose1 = np.hstack([rng.uniform(-3, 3, (B, 3)), rng.uniform(-1, 1, (B, 3))])
+    pose2 = np.hstack([rng.uniform(-3, 3, (B, 3)), rng.uniform(-1, 1, (B, 3))])
+    return s1, s2, pose1, pose2
+
+
+def run_mixed(args, world, rank, local, dev, coll_dev, dist):
+    """BASELINE configs[4]: 1M mixed-primitive pairs sharded over the ranks (class-balanced
+    round-robin, dcol_amd.dist.shard_indices), each shard solved on its GPU from
+    HBM-resident poses, then ONE all-gather of the packed per-pair record [alpha, grad(12),
+    status, iters] so every rank holds the whole batch.  The timed step = solve + pack +
+    all-gather (strong scaling: the batch is fixed as N grows)."""
+    import torch
+    from dcol_amd import Engine, alloc_outputs, spec_from_arrays
+    from dcol_amd.dist import REC, shard_indices
+    B = args.pairs if args.pairs != 100_000 else 1_000_000
+    tab = mixed_table()
+    s1, s2, p1, p2 = mixed_pairs(tab, B, seed=0)
+    cost = tab["type"][s1] * 8 + tab["type"][s2]          # class key for balanced dealing
+    idx = [shard_indices(B, r, world, cost) for r in range(world)]
+    mine = idx[rank]
+    cap = max(len(i) for i in idx)
+    eng = Engine(device=local)
+    ids = np.array([eng.register(spec_from_arrays(tab, k)) for k in range(len(tab["type"]))], np.int32)
+    plan = eng.plan(ids[s1[mine]], ids[s2[mine]])
+    d1 = torch.from_numpy(np.ascontiguousarray(p1[mine].T)).to(dev)
+    d2 = torch.from_numpy(np.ascontiguousarray(p2[mine].T)).to(dev)
+    out = alloc_outputs(len(mine), dev, want_grad=True, want_contact=False)
+    stream = torch.cuda.current_stream(dev)
+    launch = plan.bind(d1, d2, out, grad=args.grad, contact=False, stream=stream)
+    rec = torch.full((cap, REC), float("nan"), dtype=torch.float64, device=dev)
+    gathered = torch.empty((world * cap, REC), dtype=torch.float64, device=coll_dev)
+    n = len(mine)
+
+    def step():
+        launch()
+        rec[:n, 0] = out["alpha"]
+        rec[:n, 1:13] = out["grad"].T
+        rec[:n, 13] = out["status"].to(torch.float64)
+        rec[:n, 14] = out["iters"].to(torch.float64)
+        if dist is not None:
+            dist.all_gather_into_tensor(gathered, rec.to(coll_dev))
+        else:
+            gathered.copy_(rec)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=coll_dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    allrec = gathered.cpu().numpy().reshape(world, cap, REC)
+    full = np.empty((B, REC))
+    for r, ix in enumerate(idx):
+        full[ix] = allrec[r, :len(ix)]
+    status = full[:, 13].astype(np.int32)
+    line = {
+        "metric": "PDIP proximity+grad pair-solves/sec", "value": B * args.steps / elapsed, "unit": "pair-solves/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": "synthetic 1M mixed-primitive pairs sharded across GPUs + RCCL all-gather "
+                               "(BASELINE.json configs[4])", "pairs_total": B, "pairs_per_gpu": cap,
+                   "kinds": "polytope sphere cone capsule cylinder polygon; 27 supported ordered kind pairs",
+                   "gradient": args.grad, "collective": "all_gather_into_tensor of [alpha, grad(12), status, iters]",
+                   "parallelism": f"dp{world} (class-balanced shards)"},
+        "solve_stats": {"ok_frac": float(np.mean(status == 0)), "iters_mean": float(full[status == 0, 14].mean())},
+    }
+    if args.check:
+        from oracle import c_oracle
+        k = min(args.check * 8, B)
+        ref = c_oracle.run_batch(tab, s1[:k], s2[:k], p1[:k], p2[:k], want_grad=True, threads=16)
+        ok = ref["status"] == 0
+        line["parity_check"] = {
+            "pairs": int(k), "status_equal": bool(np.array_equal(status[:k], ref["status"])),
+            "alpha_ok": bool(np.all(np.abs(full[:k, 0][ok] - ref["alpha"][ok]) <= 1e-6 * np.abs(ref["alpha"][ok]) + 1e-12)),
+            "grad_ok": bool(np.all(np.abs(full[:k, 1:13][ok] - ref["grad"][ok]).max(1)
+                                   <= 1e-5 * np.maximum(np.abs(ref["grad"][ok]).max(1), 1)))}
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def scene_batches(device):
+    """Pair-solves/s of the reference's own scene batches (BASELINE configs[1], [2] and the
+    piano mover): every (knot, obstacle) pair of the reference trajectory Xref as one
+    device-resident batch with FD gradients, repeated; small launches, latency-bound."""
+    import torch
+    from altro import systems
+    from altro.constraints import ObstacleField
+    out = {}
+    for name in ("quadrotor", "coneThroughWall", "piano_mover"):
+        params, X, U = systems.initialize(name)
+        mod = systems.get(name)
+        f = ObstacleField(params["P_vic"], params["P_obs"], params["N"])
+        f.evaluate(mod.victim_poses(params, np.asarray(params["Xref"], dtype=np.float64)), True)
+        reps = 200
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            f._launch[True]()
+        torch.cuda.synchronize(device)
+        dt = (time.perf_counter() - t0) / reps
+        out[name] = {"pairs_per_batch": f.B, "ms_per_batch": 1e3 * dt, "pair_solves_per_s": f.B / dt,
+                     "launches_per_batch": f.plan.num_launches}
+    return out
 
 
 # Whole-run ALTRO wall-clock of the reference on the same problems (BASELINE.md): the
