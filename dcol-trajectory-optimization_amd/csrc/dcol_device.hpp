@@ -705,7 +705,7 @@ struct Solver {
         for (it = 0; it < max_iter; ++it) {
             DCOL_ISTAMP(it, 0);
             // ---- NT scalings, residuals, normal matrix (pdip.py:410-434)
-            double il[OR > 0 ? OR : 1];
+            double il[OR > 0 ? OR : 1];                 // orthant rows: 1 / s
             SocState so[SSA];
             double sz = 0.0, rx[N], Hm[N][N];
 #pragma unroll
@@ -717,19 +717,19 @@ struct Solver {
 #pragma unroll
             for (int k = 0; k < OR; ++k) {
                 const double sk = s[k], zk = z[k];
-                il[k] = frsqrt(sk * zk);                  // 1/lambda, lambda = sqrt(s z)
+                il[k] = frcp(sk);
                 sz = fma(vort(k) ? sk : 0.0, zk, sz);
-                const double wi = zk * il[k];
+                const double d = zk * il[k];              // W^-2 = z / s on the orthant
                 double g[N];
 #pragma unroll
                 for (int j = 0; j < N; ++j) {
                     rx[j] += G[k][j] * zk;
-                    g[j] = G[k][j] * wi;
+                    g[j] = G[k][j] * d;
                 }
 #pragma unroll
                 for (int j = 0; j < N; ++j)
 #pragma unroll
-                    for (int c = j; c < N; ++c) Hm[j][c] += g[j] * g[c];
+                    for (int c = j; c < N; ++c) Hm[j][c] += g[j] * G[k][c];
             }
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
@@ -803,7 +803,7 @@ struct Solver {
             // cp = (W^-1 ds_a) o (W dz_a)
             double cp[M];
 #pragma unroll
-            for (int k = 0; k < OR; ++k) cp[k] = (z[k] * il[k] * dsA[k]) * (s[k] * il[k] * dzA[k]);
+            for (int k = 0; k < OR; ++k) cp[k] = dsA[k] * dzA[k];     // (W^-1 ds_a) o (W dz_a), orthant
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
                 const int k0 = OR + 4 * b;
@@ -877,8 +877,7 @@ struct Solver {
         for (int j = 0; j < N; ++j) rhs[j] = 0.0;
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
-            const double lds = orth_lds(k, il, cp, smu);
-            const double t = orth_bzt(k, il, lds) * (z[k] * il[k]);    // W^-1 b~z
+            const double t = -orth_num(k, cp, smu, r[k]) * il[k];    // (W^-1 b~z)_k
 #pragma unroll
             for (int j = 0; j < N; ++j) rhs[j] += G[k][j] * t;
         }
@@ -902,15 +901,15 @@ struct Solver {
         for (int j = 0; j < N; ++j) rhs[j] -= rx[j];
         chol_solve(F, idg, rhs, dx);
     }
-    // one orthant row of the step: u = G_k dx, dz = w^-1(w^-1 u - b~z), ds = w(lds - w dz)
+    // One orthant row of the step.  With W = diag(sqrt(s/z)) and lambda = W z the
+    // reference's dz = W^-1(W^-1 u - b~z), ds = W(lds - W dz) reduce exactly to
+    //   dz = (z (u + r) + smu - cp) / s,   ds = -(s + r) - u   (u = G_k dx, r = G_k x - h_k),
+    // i.e. the primal and complementarity rows of the same Newton system, in fewer operations.
     DCOL_HD void orth_step(int k, const double* il, const double* cp, double smu, const double* dx, double& u,
                            double& dz, double& ds) const {
-        const double lds = orth_lds(k, il, cp, smu);
-        const double bzt = orth_bzt(k, il, lds);
-        const double wi = z[k] * il[k], w = s[k] * il[k];
         u = rowdot(k, dx);
-        dz = wi * (wi * u - bzt);
-        ds = w * (lds - w * dz);
+        dz = orth_num(k, cp, smu, u + r[k]) * il[k];
+        ds = -(s[k] + r[k]) - u;
     }
     DCOL_HD void soc_step(const SocState& S, int k0, const double* bzt, const double* lds, const double* dx, double* u,
                           double* dz, double* ds) const {
@@ -942,16 +941,9 @@ struct Solver {
             soc_step(so[b], OR + 4 * b, sbzt[b], slds[b], dx, u, dz + OR + 4 * b, ds + OR + 4 * b);
         }
     }
-    // orthant lambda\ds: predictor -(s z)/lambda, corrector (-(s z) - cp + smu)/lambda
-    DCOL_HD double orth_lds(int k, const double* il, const double* cp, double smu) const {
-        const double ll = s[k] * z[k];
-        const double num = cp ? (-ll - cp[k] + smu) : -ll;
-        return num * il[k];
-    }
-    // orthant b~z = w^-1 (-rz - w lds), rz = s + (G x - h)
-    DCOL_HD double orth_bzt(int k, const double* il, double lds) const {
-        const double wi = z[k] * il[k], w = s[k] * il[k];
-        return wi * (-(s[k] + r[k]) - w * lds);
+    // z v + (smu - cp) on the corrector, z v on the predictor
+    DCOL_HD double orth_num(int k, const double* cp, double smu, double v) const {
+        return cp ? fma(z[k], v, smu - cp[k]) : z[k] * v;
     }
     DCOL_HD static void soc_lds(const SocState& S, const double* cp, double smu, double* out) {
         double v[4];
