@@ -21,7 +21,7 @@ import variants  # noqa: E402
 SRC = """#include "dcol_device.hpp"
 namespace dcol {{
 template <int N, int NS, int OM, int LP>
-__global__ void __launch_bounds__(256, {w}) kb(KArgs A) {{
+__global__ void __launch_bounds__(64, {w}) kb(KArgs A) {{
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t slot = t / LP; const int q = (int)(t % LP);
     if (slot >= A.n) return;
