@@ -79,6 +79,7 @@ struct dcol_table {
     std::mutex mu;
     void* stage = nullptr;
     size_t stage_bytes = 0;
+    int simds = 1024;   // SIMDs of the device (CUs x 4): below one wave per SIMD a launch is latency-bound
     // side streams for the concurrent variant launches of mixed plans (created on first use)
     std::mutex side_mu;
     hipStream_t side[kSideStreams] = {};
@@ -156,6 +157,13 @@ int dcol_table_create(const dcol_shape_desc* shapes, int32_t n, int32_t device, 
     auto* t = new (std::nothrow) dcol_table();
     if (!t) return fail(DCOL_ERR_NOMEM, "host allocation failed");
     t->device = device;
+    {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+            t->simds = 4 * cus;
+        else
+            (void)hipGetLastError();
+    }
     t->shapes.resize(n);
     for (int32_t i = 0; i < n; ++i) {
         int rc = digest_shape(shapes[i], i, t->shapes[i], t->rows);
@@ -250,6 +258,8 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
         L.code = std::get<5>(kv.first);
         L.slot0 = (int64_t)perm.size();
         L.n = (int64_t)kv.second.size();
+        if (L.kind == 0 && !lpp_forced() && L.n * L.lpp < 64LL * t->simds)   // cannot fill the GPU
+            L.lpp = max_lpp(L.N, L.nsoc, L.omax);
         perm.insert(perm.end(), kv.second.begin(), kv.second.end());
         p->launches.push_back(L);
     }

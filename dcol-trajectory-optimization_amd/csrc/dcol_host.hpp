@@ -41,6 +41,17 @@ inline const std::map<std::pair<int, int>, std::vector<int>>& buckets() {
 
 // lanes per pair for a kernel shape: the first compiled LPP, or DCOL_LPP=<n> if that
 // alternative is compiled for the shape (A/B experiments)
+// largest compiled LPP for a kernel shape (latency choice for launches that leave the GPU
+// mostly idle)
+inline int max_lpp(int N, int nsoc, int omax) {
+    int best = 0;
+#define DCOL_MAXL(NN, NS, OM, LP, WP) \
+    if (NN == N && NS == nsoc && OM == omax && LP > best) best = LP;
+    DCOL_VARIANTS(DCOL_MAXL)
+#undef DCOL_MAXL
+    return best;
+}
+inline bool lpp_forced() { return std::getenv("DCOL_LPP") != nullptr; }
 inline int choose_lpp(int N, int nsoc, int omax) {
     static const int forced = [] {
         const char* e = std::getenv("DCOL_LPP");
