@@ -280,6 +280,18 @@ DCOL_HD void soc_solve(const SocNT& W, const double* v, double* out) {
     for (int k = 0; k < 3; ++k) out[k + 1] = W.ieta * (v[k + 1] - v[0] * W.w1[k] + c * W.w1[k]);
 }
 
+// out = W^-2 v = eta^-2 J Wbar^2 J v with Wbar^2 = [[2 w0^2 - 1, 2 w0 w1'], [2 w0 w1, I + 2 w1 w1']]
+// (uses w0^2 - |w1|^2 = 1 of the NT point; one pass instead of two soc_solve)
+DCOL_HD void soc_w2inv(const SocNT& W, const double* v, double* out) {
+    const double d = W.w1[0] * v[1] + W.w1[1] * v[2] + W.w1[2] * v[3];
+    const double e2 = W.ieta * W.ieta;
+    const double tw = 2.0 * W.w0;
+    out[0] = e2 * ((tw * W.w0 - 1.0) * v[0] - tw * d);
+    const double c = 2.0 * d - tw * v[0];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) out[k + 1] = e2 * (v[k + 1] + c * W.w1[k]);
+}
+
 // soc_cone_product(u, v), pdip.py:165-200
 DCOL_HD void soc_prod(const double* u, const double* v, double* out) {
     const double s = u[0] * v[0] + u[1] * v[1] + u[2] * v[2] + u[3] * v[3];
@@ -884,17 +896,19 @@ struct Solver {
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
             const int k0 = OR + 4 * b;
+            // W^-1 b~z = W^-1 W^-1 (-rz - W lds) = -W^-2 (s + r) - W^-1 lds   (rz = s + G x - h)
             soc_lds(so[b], cp ? cp + k0 : nullptr, smu, slds[b]);
-            double t1[4], t2[4];
-            soc_mul(so[b].W, slds[b], t1);
+            double m[4], sr[4], q[4];
+            soc_solve(so[b].W, slds[b], m);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) t1[e] = -(s[k0 + e] + r[k0 + e]) - t1[e];
-            soc_solve(so[b].W, t1, sbzt[b]);
-            soc_solve(so[b].W, sbzt[b], t2);
+            for (int e = 0; e < 4; ++e) sr[e] = s[k0 + e] + r[k0 + e];
+            soc_w2inv(so[b].W, sr, q);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sbzt[b][e] = -q[e] - m[e];
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
-                for (int j = 0; j < N; ++j) rhs[j] += G[k0 + e][j] * t2[e];
+                for (int j = 0; j < N; ++j) rhs[j] += G[k0 + e][j] * sbzt[b][e];
         }
         allsum_vec(rhs);
 #pragma unroll
@@ -911,19 +925,20 @@ struct Solver {
         dz = orth_num(k, cp, smu, u + r[k]) * il[k];
         ds = -(s[k] + r[k]) - u;
     }
-    DCOL_HD void soc_step(const SocState& S, int k0, const double* bzt, const double* lds, const double* dx, double* u,
+    // one SOC block of the step: dz = W^-1(W^-1 u - b~z) = W^-2 u - W^-1 b~z (wbz), and
+    // ds = W(lds - W dz) = -(s + r) - u (the primal row of the Newton system)
+    DCOL_HD void soc_step(const SocState& S, int k0, const double* wbz, const double* lds, const double* dx, double* u,
                           double* dz, double* ds) const {
         double t[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) u[e] = rowdot(k0 + e, dx);
-        soc_solve(S.W, u, t);
+        soc_w2inv(S.W, u, t);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) t[e] -= bzt[e];
-        soc_solve(S.W, t, dz);
-        soc_mul(S.W, dz, t);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) t[e] = lds[e] - t[e];
-        soc_mul(S.W, t, ds);
+        for (int e = 0; e < 4; ++e) {
+            dz[e] = t[e] - wbz[e];
+            ds[e] = -(s[k0 + e] + r[k0 + e]) - u[e];
+        }
+        (void)lds;
     }
     // full direction with stored ds/dz (predictor: they feed rho and the corrector's cp)
     DCOL_HD void direction(const SocState* so, const double* il, const double (&F)[N][N], const double (&idg)[N],
@@ -946,6 +961,11 @@ struct Solver {
         return cp ? fma(z[k], v, smu - cp[k]) : z[k] * v;
     }
     DCOL_HD static void soc_lds(const SocState& S, const double* cp, double smu, double* out) {
+        if (!cp) {                               // lambda \ (-lambda o lambda) = -lambda
+#pragma unroll
+            for (int e = 0; e < 4; ++e) out[e] = -S.lam[e];
+            return;
+        }
         double v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = -S.ll[e] - (cp ? cp[e] : 0.0);
