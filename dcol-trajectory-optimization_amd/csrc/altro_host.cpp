@@ -82,7 +82,8 @@ inline void dcm_from_mrp(const double* p, double Q[9]) {
                          8 * p[0] * p[2] + p[1] * a,
                          8 * p[1] * p[2] - p[0] * a,
                          dg(q1, q2)};
-    for (int i = 0; i < 9; ++i) Q[i] = M[i] / den;
+    const double iden = 1.0 / den;
+    for (int i = 0; i < 9; ++i) Q[i] = M[i] * iden;
 }
 
 // --------------------------------------------------------------------- continuous models
@@ -101,7 +102,8 @@ inline void mrp_kin(const double* p, double n2, double M[9]) {
     double S[9], SS[9];
     skew(p, S);
     mat3_mul(S, S, SS);
-    for (int i = 0; i < 9; ++i) M[i] = ((i % 4 == 0) ? 1.0 : 0.0) + 2 * (SS[i] + S[i]) / (1 + n2);
+    const double inv = 1.0 / (1 + n2);
+    for (int i = 0; i < 9; ++i) M[i] = ((i % 4 == 0) ? 1.0 : 0.0) + 2 * (SS[i] + S[i]) * inv;
 }
 
 inline void euler_rate(const dcol_altro_model& m, const double* w, const double* tau, double* wd) {
@@ -194,7 +196,7 @@ bool model_ok(const dcol_altro_model* m) {
 }
 
 // In-place lower Cholesky of the n x n SPD matrix a (row-major); false if not PD.
-bool cholesky(double* a, int n) {
+__attribute__((always_inline)) inline bool cholesky(double* a, int n) {
     for (int j = 0; j < n; ++j) {
         double d = a[j * n + j];
         for (int k = 0; k < j; ++k) d -= a[j * n + k] * a[j * n + k];
@@ -211,7 +213,7 @@ bool cholesky(double* a, int n) {
 }
 
 // Solve (L L') x = b in place for one right-hand side.
-void chol_solve(const double* L, int n, double* b) {
+__attribute__((always_inline)) inline void chol_solve(const double* L, int n, double* b) {
     for (int i = 0; i < n; ++i) {
         double s = b[i];
         for (int k = 0; k < i; ++k) s -= L[i * n + k] * b[k];
@@ -222,6 +224,103 @@ void chol_solve(const double* L, int n, double* b) {
         for (int k = i + 1; k < n; ++k) s -= L[k * n + i] * b[k];
         b[i] = s / L[i * n + i];
     }
+}
+
+// C[m x n] = A[m x p] B[p x n]; i-q-j order so the inner loop runs over contiguous
+// output columns (vectorises without reassociating any sum)
+__attribute__((always_inline)) inline void mm(int m, int p, int n, const double* A, const double* B, double* C) {
+    for (int i = 0; i < m; ++i) {
+        double* c = C + i * n;
+        for (int j = 0; j < n; ++j) c[j] = 0.0;
+        for (int q = 0; q < p; ++q) {
+            const double a = A[i * p + q];
+            const double* b = B + q * n;
+            for (int j = 0; j < n; ++j) c[j] += a * b[j];
+        }
+    }
+}
+
+// C[m x n] = A' B with A [p x m], B [p x n]
+__attribute__((always_inline)) inline void mtm(int p, int m, int n, const double* A, const double* B, double* C) {
+    for (int i = 0; i < m * n; ++i) C[i] = 0.0;
+    for (int q = 0; q < p; ++q) {
+        const double* b = B + q * n;
+        for (int i = 0; i < m; ++i) {
+            const double a = A[q * m + i];
+            double* c = C + i * n;
+            for (int j = 0; j < n; ++j) c[j] += a * b[j];
+        }
+    }
+}
+
+// Riccati recursion; NX/NU > 0 fix the sizes at compile time (fully unrolled small loops
+// for the three reference systems), 0 = runtime sizes.
+template <int NX, int NU>
+int backward_impl(int64_t T, int nx_, int nu_, const double* A, const double* B, const double* lx, const double* lu,
+                  const double* lxx, const double* luu, const double* VxT, const double* VxxT, double reg, double* K,
+                  double* k, double* dJ, int64_t* fail_knot) {
+    const int nx = NX > 0 ? NX : nx_;
+    const int nu = NU > 0 ? NU : nu_;
+    // Per knot (Vx', Vxx' = next knot's cost-to-go, P = Vxx' + reg I):
+    //   VB = Vxx' B, VA = Vxx' A;  Qu = lu + B'Vx';  Quu = luu + B'(VB + reg B);
+    //   Qux = B'(VA + reg A);  k = Quu^-1 Qu, K = Quu^-1 Qux;  Acl = A - B K;
+    //   Vxx = lxx + K' luu K + Acl' (VA - VB K);   (VA - VB K = Vxx' Acl)
+    //   Vx  = lx - K' lu + K' luu k + Acl' (Vx' - VB k)
+    double Vx[MX], Vxx[MX * MX], VA[MX * MX], VB[MX * MU], Qu[MU], Quu[MU * MU], Qux[MU * MX], L[MU * MU];
+    double Acl[MX * MX], Wm[MX * MX], LK[MU * MX], tmp[MX * MX], v1[MX], luk[MU];
+    std::memcpy(Vx, VxT, sizeof(double) * nx);
+    std::memcpy(Vxx, VxxT, sizeof(double) * nx * nx);
+    double acc = 0;
+    for (int64_t t = T - 1; t >= 0; --t) {
+        const double* At = A + t * nx * nx;
+        const double* Bt = B + t * nx * nu;
+        const double* luut = luu + t * nu * nu;
+        double* Kt = K + t * nu * nx;
+        double* kt = k + t * nu;
+        mm(nx, nx, nu, Vxx, Bt, VB);
+        mm(nx, nx, nx, Vxx, At, VA);
+        for (int i = 0; i < nx * nu; ++i) tmp[i] = VB[i] + reg * Bt[i];
+        mtm(nx, nu, nu, Bt, tmp, Quu);
+        for (int i = 0; i < nu * nu; ++i) Quu[i] += luut[i];
+        for (int i = 0; i < nx * nx; ++i) tmp[i] = VA[i] + reg * At[i];
+        mtm(nx, nu, nx, Bt, tmp, Qux);
+        mtm(nx, nu, 1, Bt, Vx, Qu);
+        for (int i = 0; i < nu; ++i) Qu[i] += lu[t * nu + i];
+        std::memcpy(L, Quu, sizeof(double) * nu * nu);
+        if (!cholesky(L, nu)) {
+            if (fail_knot) *fail_knot = t;
+            return DCOL_ALTRO_ERR_NOT_PD;
+        }
+        for (int i = 0; i < nu; ++i) kt[i] = Qu[i];
+        chol_solve(L, nu, kt);
+        for (int j = 0; j < nx; ++j) {
+            double col[MU];
+            for (int i = 0; i < nu; ++i) col[i] = Qux[i * nx + j];
+            chol_solve(L, nu, col);
+            for (int i = 0; i < nu; ++i) Kt[i * nx + j] = col[i];
+        }
+        mm(nx, nu, nx, Bt, Kt, tmp);                       // B K
+        for (int i = 0; i < nx * nx; ++i) Acl[i] = At[i] - tmp[i];
+        mm(nx, nu, nx, VB, Kt, tmp);                       // VB K
+        for (int i = 0; i < nx * nx; ++i) Wm[i] = VA[i] - tmp[i];
+        mm(nu, nu, nx, luut, Kt, LK);                      // luu K
+        mtm(nu, nx, nx, Kt, LK, tmp);                      // K' luu K
+        mtm(nx, nx, nx, Acl, Wm, Vxx);                     // Acl' Vxx' Acl
+        for (int i = 0; i < nx * nx; ++i) Vxx[i] = lxx[t * nx * nx + i] + tmp[i] + Vxx[i];
+        mm(nx, nu, 1, VB, kt, v1);                         // VB k
+        for (int i = 0; i < nx; ++i) v1[i] = Vx[i] - v1[i];
+        mm(nu, nu, 1, luut, kt, luk);
+        double a[MX], b[MX], c[MX];
+        mtm(nu, nx, 1, Kt, lu + t * nu, a);
+        mtm(nu, nx, 1, Kt, luk, b);
+        mtm(nx, nx, 1, Acl, v1, c);
+        for (int i = 0; i < nx; ++i) Vx[i] = lx[t * nx + i] - a[i] + b[i] + c[i];
+        double d = 0;
+        for (int i = 0; i < nu; ++i) d += Qu[i] * kt[i];
+        acc += d;
+    }
+    *dJ = acc;
+    return DCOL_ALTRO_OK;
 }
 
 }  // namespace
@@ -270,126 +369,10 @@ int dcol_altro_backward(int64_t T, int32_t nx, int32_t nu, const double* A, cons
                         const double* VxxT, double reg, double* K, double* k, double* dJ, int64_t* fail_knot) {
     if (T < 0 || nx <= 0 || nx > MX || nu <= 0 || nu > MU || !VxT || !VxxT || !dJ) return DCOL_ALTRO_ERR_ARG;
     if (T > 0 && (!A || !B || !lx || !lu || !lxx || !luu || !K || !k)) return DCOL_ALTRO_ERR_ARG;
-    double Vx[MX], Vxx[MX * MX], P[MX * MX];
-    double PB[MX * MU], PA[MX * MX], Qu[MU], Quu[MU * MU], Qux[MU * MX], L[MU * MU];
-    double Acl[MX * MX], VA[MX * MX], LK[MU * MX], t1[MX], t2[MX], nVx[MX], nVxx[MX * MX];
-    std::memcpy(Vx, VxT, sizeof(double) * nx);
-    std::memcpy(Vxx, VxxT, sizeof(double) * nx * nx);
-    double acc = 0;
-    for (int64_t t = T - 1; t >= 0; --t) {
-        const double* At = A + t * nx * nx;
-        const double* Bt = B + t * nx * nu;
-        const double* lxt = lx + t * nx;
-        const double* lut = lu + t * nu;
-        const double* lxxt = lxx + t * nx * nx;
-        const double* luut = luu + t * nu * nu;
-        double* Kt = K + t * nu * nx;
-        double* kt = k + t * nu;
-        // P = Vxx' + reg I ; PB = P B ; PA = P A
-        for (int i = 0; i < nx; ++i)
-            for (int j = 0; j < nx; ++j) P[i * nx + j] = Vxx[i * nx + j] + (i == j ? reg : 0.0);
-        for (int i = 0; i < nx; ++i) {
-            for (int j = 0; j < nu; ++j) {
-                double s = 0;
-                for (int q = 0; q < nx; ++q) s += P[i * nx + q] * Bt[q * nu + j];
-                PB[i * nu + j] = s;
-            }
-            for (int j = 0; j < nx; ++j) {
-                double s = 0;
-                for (int q = 0; q < nx; ++q) s += P[i * nx + q] * At[q * nx + j];
-                PA[i * nx + j] = s;
-            }
-        }
-        // Qu = lu + B'Vx' ; Quu = luu + B'PB ; Qux = B'PA
-        for (int i = 0; i < nu; ++i) {
-            double s = 0;
-            for (int q = 0; q < nx; ++q) s += Bt[q * nu + i] * Vx[q];
-            Qu[i] = lut[i] + s;
-            for (int j = 0; j < nu; ++j) {
-                double r = 0;
-                for (int q = 0; q < nx; ++q) r += Bt[q * nu + i] * PB[q * nu + j];
-                Quu[i * nu + j] = luut[i * nu + j] + r;
-            }
-            for (int j = 0; j < nx; ++j) {
-                double r = 0;
-                for (int q = 0; q < nx; ++q) r += Bt[q * nu + i] * PA[q * nx + j];
-                Qux[i * nx + j] = r;
-            }
-        }
-        std::memcpy(L, Quu, sizeof(double) * nu * nu);
-        if (!cholesky(L, nu)) {
-            if (fail_knot) *fail_knot = t;
-            return DCOL_ALTRO_ERR_NOT_PD;
-        }
-        for (int i = 0; i < nu; ++i) kt[i] = Qu[i];
-        chol_solve(L, nu, kt);
-        for (int j = 0; j < nx; ++j) {
-            double col[MU];
-            for (int i = 0; i < nu; ++i) col[i] = Qux[i * nx + j];
-            chol_solve(L, nu, col);
-            for (int i = 0; i < nu; ++i) Kt[i * nx + j] = col[i];
-        }
-        // Acl = A - B K
-        for (int i = 0; i < nx; ++i)
-            for (int j = 0; j < nx; ++j) {
-                double s = 0;
-                for (int q = 0; q < nu; ++q) s += Bt[i * nu + q] * Kt[q * nx + j];
-                Acl[i * nx + j] = At[i * nx + j] - s;
-            }
-        // Vxx = lxx + K' luu K + Acl' Vxx' Acl
-        for (int i = 0; i < nu; ++i)
-            for (int j = 0; j < nx; ++j) {
-                double s = 0;
-                for (int q = 0; q < nu; ++q) s += luut[i * nu + q] * Kt[q * nx + j];
-                LK[i * nx + j] = s;
-            }
-        for (int i = 0; i < nx; ++i)
-            for (int j = 0; j < nx; ++j) {
-                double s = 0;
-                for (int q = 0; q < nx; ++q) s += Vxx[i * nx + q] * Acl[q * nx + j];
-                VA[i * nx + j] = s;
-            }
-        for (int i = 0; i < nx; ++i)
-            for (int j = 0; j < nx; ++j) {
-                double a = 0, b = 0;
-                for (int q = 0; q < nu; ++q) a += Kt[q * nx + i] * LK[q * nx + j];
-                for (int q = 0; q < nx; ++q) b += Acl[q * nx + i] * VA[q * nx + j];
-                nVxx[i * nx + j] = lxxt[i * nx + j] + a + b;
-            }
-        // Vx = lx - K' lu + K' luu k + Acl' (Vx' - Vxx' B k)
-        for (int i = 0; i < nx; ++i) {
-            double s = 0;
-            for (int q = 0; q < nu; ++q) s += Bt[i * nu + q] * kt[q];
-            t1[i] = s;   // B k
-        }
-        for (int i = 0; i < nx; ++i) {
-            double s = 0;
-            for (int q = 0; q < nx; ++q) s += Vxx[i * nx + q] * t1[q];
-            t2[i] = Vx[i] - s;
-        }
-        double luk[MU];
-        for (int i = 0; i < nu; ++i) {
-            double s = 0;
-            for (int q = 0; q < nu; ++q) s += luut[i * nu + q] * kt[q];
-            luk[i] = s;
-        }
-        for (int i = 0; i < nx; ++i) {
-            double a = 0, b = 0, c = 0;
-            for (int q = 0; q < nu; ++q) {
-                a += Kt[q * nx + i] * lut[q];
-                b += Kt[q * nx + i] * luk[q];
-            }
-            for (int q = 0; q < nx; ++q) c += Acl[q * nx + i] * t2[q];
-            nVx[i] = lxt[i] - a + b + c;
-        }
-        double d = 0;
-        for (int i = 0; i < nu; ++i) d += Qu[i] * kt[i];
-        acc += d;
-        std::memcpy(Vx, nVx, sizeof(double) * nx);
-        std::memcpy(Vxx, nVxx, sizeof(double) * nx * nx);
-    }
-    *dJ = acc;
-    return DCOL_ALTRO_OK;
+    if (nx == 6 && nu == 3) return backward_impl<6, 3>(T, nx, nu, A, B, lx, lu, lxx, luu, VxT, VxxT, reg, K, k, dJ, fail_knot);
+    if (nx == 12 && nu == 4) return backward_impl<12, 4>(T, nx, nu, A, B, lx, lu, lxx, luu, VxT, VxxT, reg, K, k, dJ, fail_knot);
+    if (nx == 12 && nu == 6) return backward_impl<12, 6>(T, nx, nu, A, B, lx, lu, lxx, luu, VxT, VxxT, reg, K, k, dJ, fail_knot);
+    return backward_impl<0, 0>(T, nx, nu, A, B, lx, lu, lxx, luu, VxT, VxxT, reg, K, k, dJ, fail_knot);
 }
 
 int dcol_altro_rollout(const dcol_altro_model* m, int64_t T, const double* X, const double* U, const double* K,

@@ -100,7 +100,7 @@ def _spd(rng, n, shift):
     return M @ M.T + shift * np.eye(n)
 
 
-@pytest.mark.parametrize("nx,nu,T", [(6, 3, 12), (12, 4, 20), (12, 6, 7)])
+@pytest.mark.parametrize("nx,nu,T", [(6, 3, 12), (12, 4, 20), (12, 6, 7), (7, 2, 9)])   # last: generic sizes
 def test_riccati_matches_reference_math(nx, nu, T):
     from oracle import altro_oracle as ao
     rng = np.random.default_rng(nx * 100 + nu)
