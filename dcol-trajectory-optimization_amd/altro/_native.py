@@ -29,6 +29,13 @@ class Model(ctypes.Structure):
                 ("km", c_double), ("u_scale", c_double)]
 
 
+class Problem(ctypes.Structure):
+    """struct dcol_altro_problem (pointers into arrays kept alive by `keep`)"""
+    _fields_ = [("N", c_int32), ("nx", c_int32), ("nu", c_int32), ("ncx", c_int32), ("Q", c_void_p),
+                ("R", c_void_p), ("Qf", c_void_p), ("Xref", c_void_p), ("Uref", c_void_p), ("u_min", c_void_p),
+                ("u_max", c_void_p)]
+
+
 SIGNATURES = {
     "dcol_altro_abi_version": (c_int32, []),
     "dcol_altro_dynamics": (c_int, [POINTER(Model), c_int64, c_void_p, c_void_p, c_void_p]),
@@ -38,6 +45,13 @@ SIGNATURES = {
                                     POINTER(c_int64)]),
     "dcol_altro_rollout": (c_int, [POINTER(Model), c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_double,
                                    c_void_p, c_void_p]),
+    "dcol_altro_cost": (c_int, [POINTER(Problem), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_double, POINTER(c_double)]),
+    "dcol_altro_stage_terms": (c_int, [POINTER(Problem), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_double, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p]),
+    "dcol_altro_victim_poses": (c_int, [POINTER(Model), c_int64, c_void_p, c_void_p]),
+    "dcol_altro_constraint_jacobian": (c_int, [POINTER(Model), c_int64, c_int32, c_void_p, c_void_p, c_void_p]),
 }
 
 _lib = None
@@ -150,3 +164,56 @@ def rollout(model: Model, X, U, K, k, a):
     _check(load().dcol_altro_rollout(ctypes.byref(model), T, _ptr(X), _ptr(U), _ptr(K), _ptr(k), float(a), _ptr(Xn),
                                      _ptr(Un)), "dcol_altro_rollout")
     return Xn, Un
+
+
+def make_problem(N, nx, nu, ncx, Q, R, Qf, Xref, Uref, u_min, u_max) -> Problem:
+    """struct dcol_altro_problem over contiguous float64 copies (held in .keep)."""
+    arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (Q, R, Qf, Xref, Uref, u_min, u_max)]
+    shapes = [(nx, nx), (nu, nu), (nx, nx), (N, nx), (N - 1, nu), (nu,), (nu,)]
+    arrs = [a.reshape(sh) for a, sh in zip(arrs, shapes)]
+    p = Problem(int(N), int(nx), int(nu), int(ncx), *[_ptr(a) for a in arrs])
+    p.keep = arrs
+    return p
+
+
+def cost(prob: Problem, X, U, hx, mu, mux, lam, rho):
+    """Augmented-Lagrangian objective (ALTRO.py compute_total_cost)."""
+    X, U, hx, mu, mux, lam = (_c(a) for a in (X, U, hx, mu, mux, lam))
+    J = c_double()
+    _check(load().dcol_altro_cost(ctypes.byref(prob), _ptr(X), _ptr(U), _ptr(hx), _ptr(mu), _ptr(mux), _ptr(lam),
+                                  float(rho), ctypes.byref(J)), "dcol_altro_cost")
+    return J.value
+
+
+def stage_terms(prob: Problem, X, U, hx, Gx, mu, mux, lam, rho):
+    """-> (lx [N-1,nx], lu [N-1,nu], lxx [N-1,nx,nx], luu [N-1,nu,nu], VxT [nx], VxxT [nx,nx])."""
+    N, nx, nu = prob.N, prob.nx, prob.nu
+    X, U, hx, Gx, mu, mux, lam = (_c(a) for a in (X, U, hx, Gx, mu, mux, lam))
+    lx = np.empty((N - 1, nx))
+    lu = np.empty((N - 1, nu))
+    lxx = np.empty((N - 1, nx, nx))
+    luu = np.empty((N - 1, nu, nu))
+    VxT = np.empty(nx)
+    VxxT = np.empty((nx, nx))
+    _check(load().dcol_altro_stage_terms(ctypes.byref(prob), _ptr(X), _ptr(U), _ptr(hx), _ptr(Gx), _ptr(mu),
+                                         _ptr(mux), _ptr(lam), float(rho), _ptr(lx), _ptr(lu), _ptr(lxx), _ptr(luu),
+                                         _ptr(VxT), _ptr(VxxT)), "dcol_altro_stage_terms")
+    return lx, lu, lxx, luu, VxT, VxxT
+
+
+def victim_poses(model: Model, X):
+    X = _c(X).reshape(-1, model.nx)
+    P = np.empty((X.shape[0], 6))
+    _check(load().dcol_altro_victim_poses(ctypes.byref(model), X.shape[0], _ptr(X), _ptr(P)),
+           "dcol_altro_victim_poses")
+    return P
+
+
+def constraint_jacobian(model: Model, X, dalpha):
+    X = _c(X).reshape(-1, model.nx)
+    N = X.shape[0]
+    D = _c(dalpha).reshape(N, -1, 12)
+    G = np.empty((N, D.shape[1], model.nx))
+    _check(load().dcol_altro_constraint_jacobian(ctypes.byref(model), N, D.shape[1], _ptr(X), _ptr(D), _ptr(G)),
+           "dcol_altro_constraint_jacobian")
+    return G

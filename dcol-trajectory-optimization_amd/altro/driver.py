@@ -15,7 +15,8 @@ reference optimizer (ALTRO.py:365-488); what changes is how the work is issued:
     search trial, rollout + N x n_obs solves        one native rollout + ONE alpha batch
     (:183-239)
   AL dual update re-solves N x n_obs (:444-470)    reuses the accepted trial's alpha
-  cost / AL terms per knot (:103-145, :259-300)    vectorised over knots (NumPy)
+  cost / AL terms per knot (:103-145, :259-300)    dcol_altro_cost / dcol_altro_stage_terms,
+                                                   native, whole trajectory per call
 
 Every reuse is of a value the reference recomputes from identical inputs, so the
 iterates are the reference's up to floating-point rounding (tests/test_altro.py pins them
@@ -83,39 +84,27 @@ def _masked(dual, h):
 
 
 class _Problem:
-    """Array views of a reference params dict."""
+    """A reference params dict as native structs (dcol_altro_model / dcol_altro_problem)."""
 
     def __init__(self, params):
         self.params = params
         self.sys = _systems.get(params["system"])
         self.N, self.nx, self.nu = int(params["N"]), int(params["nx"]), int(params["nu"])
-        self.Q = np.asarray(params["Q"], dtype=np.float64)
-        self.R = np.asarray(params["R"], dtype=np.float64)
-        self.Qf = np.asarray(params["Qf"], dtype=np.float64)
+        self.ncx = len(params["P_obs"])
         self.Xref = np.asarray(params["Xref"], dtype=np.float64).reshape(-1, self.nx)[: self.N]
-        self.Uref = np.asarray(params["Uref"], dtype=np.float64).reshape(-1, self.nu)[: self.N - 1]
         self.u_max = np.asarray(params["u_max"], dtype=np.float64)
         self.u_min = np.asarray(params["u_min"], dtype=np.float64)
         self.model = self.sys.native_model(params)
-        I = np.eye(self.nu)
-        self.Gu = np.vstack([I, -I])                       # d h_u / d u (constant)
+        self.prob = _native.make_problem(
+            self.N, self.nx, self.nu, self.ncx, params["Q"], params["R"], params["Qf"], self.Xref,
+            np.asarray(params["Uref"], dtype=np.float64).reshape(-1, self.nu)[: self.N - 1], self.u_min, self.u_max)
 
     def hu(self, U):
         return np.concatenate([U - self.u_max, -U + self.u_min], axis=1)
 
-    def cost(self, X, U, hx, hu, mu, mux, lam, rho):
-        """compute_total_cost (ALTRO.py:103-145), terms summed in the reference's order."""
-        dx = X - self.Xref
-        du = U - self.Uref
-        run = 0.5 * np.einsum("ti,ij,tj->t", dx[:-1], self.Q, dx[:-1]) + 0.5 * np.einsum("ti,ij,tj->t", du, self.R, du)
-        mu_mask = _masked(mu, hu)
-        x_mask = _masked(mux, hx)
-        alu = np.einsum("ti,ti->t", mu, hu) + 0.5 * rho * np.einsum("ti,ti,ti->t", hu, mu_mask, hu)
-        alx = np.einsum("ti,ti->t", mux, hx) + 0.5 * rho * np.einsum("ti,ti,ti->t", hx, x_mask, hx)
-        g = X[-1] - self.Xref[-1]
-        tail = [0.5 * dx[-1] @ self.Qf @ dx[-1], alx[-1], lam @ g + 0.5 * rho * (g @ g)]
-        terms = np.concatenate([np.stack([run, alu, alx[:-1]], axis=1).ravel(), tail])
-        return float(np.cumsum(terms)[-1])
+    def cost(self, X, U, hx, mu, mux, lam, rho):
+        """compute_total_cost (ALTRO.py:103-145)."""
+        return _native.cost(self.prob, X, U, hx, mu, mux, lam, rho)
 
 
 def _print_iter(itr, J, dJ, kmax, a, reg, rho):
@@ -143,7 +132,7 @@ def solve(params, X, U, prox=None, engine=None, verbose=True) -> AltroResult:
         prox = ObstacleField(params["P_vic"], params["P_obs"], N, engine=engine)
     evaluate = _Timed(prox)
     t_start = time.perf_counter()          # one-time set-up (shape table, plan, warm-up) excluded
-    ncx = len(params["P_obs"])
+    ncx = P.ncx
     if int(params.get("ncx", ncx)) != ncx or int(params.get("ncu", 2 * nu)) != 2 * nu:
         raise AssertionError("ncx / ncu do not match the problem")
 
@@ -163,32 +152,20 @@ def solve(params, X, U, prox=None, engine=None, verbose=True) -> AltroResult:
         res.reg.append(reg)
         res.rho.append(rho)
         # ---------------------------------------------------------------- backward pass
-        alpha, Jp = evaluate(P.sys.victim_poses(params, X), True)
+        alpha, Jp = evaluate(_native.victim_poses(P.model, X), True)
         hx = 1 - alpha
-        Gx = P.sys.state_jacobian(params, X, Jp)                    # [N, ncx, nx]
-        hu = P.hu(U)
+        Gx = _native.constraint_jacobian(P.model, X, Jp)            # [N, ncx, nx]
         A, B = _native.jacobians(P.model, X, U)
-        dx = X - P.Xref
-        du = U - P.Uref
-        xm = _masked(mux, hx)
-        um = _masked(mu, hu)
-        GxT = np.swapaxes(Gx, 1, 2)                                 # [N, nx, ncx]
-        lx = dx @ P.Q.T + np.matmul(GxT, (mux + rho * (xm * hx))[:, :, None])[:, :, 0]
-        lxx = P.Q + rho * np.matmul(GxT * xm[:, None, :], Gx)
-        lu = du @ P.R.T + (mu + rho * (um * hu)) @ P.Gu
-        luu = P.R + rho * np.matmul(P.Gu.T * um[:, None, :], P.Gu)
-        g = X[-1] - P.Xref[-1]
-        VxT = P.Qf @ dx[-1] + Gx[-1].T @ (mux[-1] + rho * (xm[-1] * hx[-1])) + (lam + rho * g)
-        VxxT = P.Qf + rho * (Gx[-1].T * xm[-1]) @ Gx[-1] + rho * np.eye(nx)
-        K, k, dJ = _native.backward(A, B, lx[:-1], lu, lxx[:-1], luu, VxT, VxxT, reg)
+        lx, lu, lxx, luu, VxT, VxxT = _native.stage_terms(P.prob, X, U, hx, Gx, mu, mux, lam, rho)
+        K, k, dJ = _native.backward(A, B, lx, lu, lxx, luu, VxT, VxxT, reg)
         # ---------------------------------------------------------------- forward pass
-        old = P.cost(X, U, hx, hu, mu, mux, lam, rho)
+        old = P.cost(X, U, hx, mu, mux, lam, rho)
         a, J, accepted = 1.0, old, False
         for _ in range(int(params["max_linesearch_iters"])):
             Xn, Un = _native.rollout(P.model, X, U, K, k, a)
-            an, _ = evaluate(P.sys.victim_poses(params, Xn), False)
+            an, _ = evaluate(_native.victim_poses(P.model, Xn), False)
             hxn = 1 - an
-            new = P.cost(Xn, Un, hxn, P.hu(Un), mu, mux, lam, rho)
+            new = P.cost(Xn, Un, hxn, mu, mux, lam, rho)
             if new < old:
                 X, U, J, accepted, hx_cur = Xn, Un, new, True, hxn
                 break

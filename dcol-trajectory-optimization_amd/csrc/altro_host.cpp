@@ -397,3 +397,197 @@ int dcol_altro_rollout(const dcol_altro_model* m, int64_t T, const double* X, co
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- AL objective pieces
+namespace {
+
+bool problem_ok(const dcol_altro_problem* p) {
+    return p && p->N >= 2 && p->nx > 0 && p->nx <= MX && p->nu > 0 && p->nu <= MU && p->ncx >= 0 && p->Q && p->R &&
+           p->Qf && p->Xref && p->Uref && p->u_min && p->u_max;
+}
+
+// x' M x for a row-major n x n M
+inline double quad(const double* M, const double* x, int n) {
+    double acc = 0.0;
+    for (int i = 0; i < n; ++i) {
+        double r = 0.0;
+        for (int j = 0; j < n; ++j) r += M[i * n + j] * x[j];
+        acc += x[i] * r;
+    }
+    return acc;
+}
+
+// AL term of one constraint block: dual . h + rho/2 sum_{active} h^2, active = dual > 0 or h > 0
+inline double al_term(const double* dual, const double* h, int n, double rho) {
+    double d = 0.0, q = 0.0;
+    for (int i = 0; i < n; ++i) {
+        d += dual[i] * h[i];
+        if (dual[i] > 0 || h[i] > 0) q += h[i] * h[i];
+    }
+    return d + 0.5 * rho * q;
+}
+
+inline void control_h(const dcol_altro_problem* p, const double* u, double* h) {
+    for (int i = 0; i < p->nu; ++i) {
+        h[i] = u[i] - p->u_max[i];
+        h[p->nu + i] = -u[i] + p->u_min[i];
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int dcol_altro_cost(const dcol_altro_problem* p, const double* X, const double* U, const double* hx, const double* mu,
+                    const double* mux, const double* lam, double rho, double* J) {
+    if (!problem_ok(p) || !X || !U || !mu || !mux || !lam || !J || (p->ncx > 0 && !hx)) return DCOL_ALTRO_ERR_ARG;
+    const int N = p->N, nx = p->nx, nu = p->nu, nc = p->ncx;
+    double cost = 0.0, dx[MX], du[MU], hu[2 * MU];
+    for (int t = 0; t < N - 1; ++t) {
+        for (int i = 0; i < nx; ++i) dx[i] = X[t * nx + i] - p->Xref[t * nx + i];
+        for (int i = 0; i < nu; ++i) du[i] = U[t * nu + i] - p->Uref[t * nu + i];
+        cost += 0.5 * quad(p->Q, dx, nx) + 0.5 * quad(p->R, du, nu);
+        control_h(p, U + t * nu, hu);
+        cost += al_term(mu + t * 2 * nu, hu, 2 * nu, rho);
+        cost += al_term(mux + t * nc, hx + t * nc, nc, rho);
+    }
+    const double* xN = X + (N - 1) * nx;
+    const double* rN = p->Xref + (N - 1) * nx;
+    for (int i = 0; i < nx; ++i) dx[i] = xN[i] - rN[i];
+    cost += 0.5 * quad(p->Qf, dx, nx);
+    cost += al_term(mux + (N - 1) * nc, hx + (N - 1) * nc, nc, rho);
+    double lg = 0.0, gg = 0.0;
+    for (int i = 0; i < nx; ++i) {
+        lg += lam[i] * dx[i];
+        gg += dx[i] * dx[i];
+    }
+    cost += lg + 0.5 * rho * gg;
+    *J = cost;
+    return DCOL_ALTRO_OK;
+}
+
+int dcol_altro_stage_terms(const dcol_altro_problem* p, const double* X, const double* U, const double* hx,
+                           const double* Gx, const double* mu, const double* mux, const double* lam, double rho,
+                           double* lx, double* lu, double* lxx, double* luu, double* VxT, double* VxxT) {
+    if (!problem_ok(p) || !X || !U || !mu || !mux || !lam || !lx || !lu || !lxx || !luu || !VxT || !VxxT ||
+        (p->ncx > 0 && (!hx || !Gx)))
+        return DCOL_ALTRO_ERR_ARG;
+    const int N = p->N, nx = p->nx, nu = p->nu, nc = p->ncx;
+    double hu[2 * MU], w[64], mk[64];
+    if (nc > 64) return DCOL_ALTRO_ERR_ARG;
+    // collision terms of knot t into (gx, gxx): gx += Gx' (mux + rho m h), gxx += rho Gx' diag(m) Gx
+    auto collision = [&](int t, double* gx, double* gxx) {
+        const double* h = hx + t * nc;
+        const double* d = mux + t * nc;
+        const double* G = Gx + (int64_t)t * nc * nx;
+        for (int c = 0; c < nc; ++c) {
+            mk[c] = (d[c] > 0 || h[c] > 0) ? 1.0 : 0.0;
+            w[c] = d[c] + rho * (mk[c] * h[c]);
+        }
+        for (int c = 0; c < nc; ++c) {
+            const double* g = G + c * nx;
+            for (int i = 0; i < nx; ++i) gx[i] += g[i] * w[c];
+            if (mk[c] != 0.0) {
+                const double rm = rho * mk[c];
+                for (int i = 0; i < nx; ++i) {
+                    const double gi = rm * g[i];
+                    for (int j = 0; j < nx; ++j) gxx[i * nx + j] += gi * g[j];
+                }
+            }
+        }
+    };
+    for (int t = 0; t < N - 1; ++t) {
+        double* lxt = lx + t * nx;
+        double* lut = lu + t * nu;
+        double* lxxt = lxx + (int64_t)t * nx * nx;
+        double* luut = luu + (int64_t)t * nu * nu;
+        for (int i = 0; i < nx; ++i) {
+            double r = 0.0;
+            for (int j = 0; j < nx; ++j) r += p->Q[i * nx + j] * (X[t * nx + j] - p->Xref[t * nx + j]);
+            lxt[i] = r;
+        }
+        for (int i = 0; i < nx * nx; ++i) lxxt[i] = p->Q[i];
+        collision(t, lxt, lxxt);
+        for (int i = 0; i < nu; ++i) {
+            double r = 0.0;
+            for (int j = 0; j < nu; ++j) r += p->R[i * nu + j] * (U[t * nu + j] - p->Uref[t * nu + j]);
+            lut[i] = r;
+        }
+        for (int i = 0; i < nu * nu; ++i) luut[i] = p->R[i];
+        control_h(p, U + t * nu, hu);
+        const double* mt = mu + t * 2 * nu;
+        for (int i = 0; i < nu; ++i) {                  // Gu = [I; -I]
+            const double m1 = (mt[i] > 0 || hu[i] > 0) ? 1.0 : 0.0;
+            const double m2 = (mt[nu + i] > 0 || hu[nu + i] > 0) ? 1.0 : 0.0;
+            lut[i] += (mt[i] + rho * (m1 * hu[i])) - (mt[nu + i] + rho * (m2 * hu[nu + i]));
+            luut[i * nu + i] += rho * (m1 + m2);
+        }
+    }
+    const int T = N - 1;
+    const double* xN = X + T * nx;
+    const double* rN = p->Xref + T * nx;
+    for (int i = 0; i < nx; ++i) {
+        double r = 0.0;
+        for (int j = 0; j < nx; ++j) r += p->Qf[i * nx + j] * (xN[j] - rN[j]);
+        VxT[i] = r;
+    }
+    for (int i = 0; i < nx * nx; ++i) VxxT[i] = p->Qf[i];
+    collision(T, VxT, VxxT);
+    for (int i = 0; i < nx; ++i) {
+        VxT[i] += lam[i] + rho * (xN[i] - rN[i]);
+        VxxT[i * nx + i] += rho;
+    }
+    return DCOL_ALTRO_OK;
+}
+
+int dcol_altro_victim_poses(const dcol_altro_model* m, int64_t N, const double* X, double* poses) {
+    if (!model_ok(m) || N < 0 || (N > 0 && (!X || !poses))) return DCOL_ALTRO_ERR_ARG;
+    const int nx = m->nx;
+    for (int64_t t = 0; t < N; ++t) {
+        const double* x = X + t * nx;
+        double* q = poses + 6 * t;
+        if (m->system == DCOL_SYS_PIANO) {      // r = (x0, x1, 0), p = (0, 0, 1) tan(theta / 4)
+            const double tq = std::tan(x[4] / 4);
+            q[0] = x[0]; q[1] = x[1]; q[2] = 0.0;
+            q[3] = 0.0 * tq; q[4] = 0.0 * tq; q[5] = tq;
+        } else {                                // r = x[0:3], p = x[6:9]
+            for (int i = 0; i < 3; ++i) {
+                q[i] = x[i];
+                q[3 + i] = x[6 + i];
+            }
+        }
+    }
+    return DCOL_ALTRO_OK;
+}
+
+int dcol_altro_constraint_jacobian(const dcol_altro_model* m, int64_t N, int32_t ncx, const double* X,
+                                   const double* dalpha, double* Gx) {
+    if (!model_ok(m) || N < 0 || ncx < 0 || (N > 0 && ncx > 0 && (!X || !dalpha || !Gx))) return DCOL_ALTRO_ERR_ARG;
+    const int nx = m->nx;
+    for (int64_t t = 0; t < N; ++t) {
+        const double* x = X + t * nx;
+        double c = 0.0;
+        if (m->system == DCOL_SYS_PIANO) {      // dp/dtheta = (0, 0, 1) / (4 cos^2(theta / 4))
+            const double cs = std::cos(x[4] / 4);
+            c = 1 / (4 * (cs * cs));
+        }
+        for (int k = 0; k < ncx; ++k) {
+            const double* J = dalpha + (t * ncx + k) * 12;
+            double* g = Gx + (t * ncx + k) * nx;
+            for (int i = 0; i < nx; ++i) g[i] = 0.0;
+            if (m->system == DCOL_SYS_PIANO) {
+                g[0] = -J[0];
+                g[1] = -J[1];
+                g[4] = -(J[3] * 0.0 + J[4] * 0.0 + J[5] * c);
+            } else {
+                for (int i = 0; i < 3; ++i) {
+                    g[i] = -J[i];
+                    g[6 + i] = -J[3 + i];
+                }
+            }
+        }
+    }
+    return DCOL_ALTRO_OK;
+}
+
+}  // extern "C"

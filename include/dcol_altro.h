@@ -15,6 +15,10 @@
  *     (Quu = luu + B'(Vxx+reg I)B, scipy cho_factor/solve)
  *   ALTRO.py forward_pass rollout :214-217                     dcol_altro_rollout()
  *     (U - K(Xn - X) - a k, then discrete_dynamics)
+ *   ALTRO.py compute_total_cost :103-145                       dcol_altro_cost()
+ *   ALTRO.py backward_pass stage / terminal terms :254-300     dcol_altro_stage_terms()
+ *   systems/<sys>.py pose map and d(1-alpha)/dx chain rule     dcol_altro_victim_poses(),
+ *     (piano_mover.py:60-61, :83-95; quad :127-128, :159-168)  dcol_altro_constraint_jacobian()
  *
  * Row-major float64 arrays; plain pointers and sizes; no allocation visible to callers.
  * Every entry point returns DCOL_ALTRO_OK or a negative DCOL_ALTRO_ERR_*.
@@ -56,6 +60,19 @@ typedef struct dcol_altro_model {
     double u_scale;     /* PIANO: angular acceleration = u[2] / u_scale (reference: 100)       */
 } dcol_altro_model;
 
+/* Cost and AL data of one trajectory-optimisation problem (ALTRO.py params).  u bounds
+ * give the control constraints h_u = [u - u_max, -u + u_min] (2 nu rows per knot). */
+typedef struct dcol_altro_problem {
+    int32_t N, nx, nu, ncx; /* knots, state / control dims, collision constraints per knot      */
+    const double* Q;        /* [nx, nx] stage state weight                                        */
+    const double* R;        /* [nu, nu] stage control weight                                      */
+    const double* Qf;       /* [nx, nx] terminal weight                                           */
+    const double* Xref;     /* [N, nx]                                                            */
+    const double* Uref;     /* [N-1, nu]                                                          */
+    const double* u_min;    /* [nu]                                                               */
+    const double* u_max;    /* [nu]                                                               */
+} dcol_altro_problem;
+
 int32_t dcol_altro_abi_version(void);
 
 /* Xn[i] = RK4(X[i], U[i]) for i < M (independent states).  X [M, nx], U [M, nu]. */
@@ -78,6 +95,28 @@ int dcol_altro_backward(int64_t T, int32_t nx, int32_t nu, const double* A, cons
  * Xn[0] = X[0], t < T.  X [T+1, nx], U [T, nu]. */
 int dcol_altro_rollout(const dcol_altro_model* m, int64_t T, const double* X, const double* U, const double* K,
                        const double* k, double a, double* Xn, double* Un);
+
+/* Augmented-Lagrangian objective of a trajectory (compute_total_cost): stage costs, AL
+ * terms of the control bounds and of the collision constraints hx [N, ncx] with duals
+ * mu [N-1, 2 nu], mux [N, ncx] (active set: dual > 0 or h > 0), terminal cost and the goal
+ * constraint x_N - xref_N with dual lam [nx].  Sums in the reference's order. */
+int dcol_altro_cost(const dcol_altro_problem* p, const double* X, const double* U, const double* hx,
+                    const double* mu, const double* mux, const double* lam, double rho, double* J);
+
+/* Derivatives of the same objective for the backward pass: per knot t < N-1 lx [nx], lu [nu],
+ * lxx [nx, nx], luu [nu, nu] (Gx [N, ncx, nx] = d hx / d x), and the terminal cost-to-go
+ * VxT [nx], VxxT [nx, nx]. */
+int dcol_altro_stage_terms(const dcol_altro_problem* p, const double* X, const double* U, const double* hx,
+                           const double* Gx, const double* mu, const double* mux, const double* lam, double rho,
+                           double* lx, double* lu, double* lxx, double* luu, double* VxT, double* VxxT);
+
+/* Victim pose per knot, [N, 6] = (r, p MRP), from the state (system-specific map). */
+int dcol_altro_victim_poses(const dcol_altro_model* m, int64_t N, const double* X, double* poses);
+
+/* d(1 - alpha)/dx [N, ncx, nx] from d alpha / d[r1, p1, r2, p2] [N, ncx, 12] (chain rule
+ * through the pose map; the victim is primitive 1). */
+int dcol_altro_constraint_jacobian(const dcol_altro_model* m, int64_t N, int32_t ncx, const double* X,
+                                   const double* dalpha, double* Gx);
 
 #ifdef __cplusplus
 }

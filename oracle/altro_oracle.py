@@ -110,3 +110,62 @@ def rollout(step, X, U, K, k, a):
         Un[t] = U[t] - K[t] @ (Xn[t] - X[t]) - a * k[t]
         Xn[t + 1] = step(Xn[t], Un[t])
     return Xn, Un
+
+
+def _mask(dual, h):
+    return np.diag([(d > 0 or v > 0) for d, v in zip(dual, h)]).astype(float)   # ALTRO.py:16-31
+
+
+def al_cost(Q, R, Qf, Xref, Uref, u_min, u_max, X, U, hx, mu, mux, lam, rho):
+    """compute_total_cost, ALTRO.py:103-145 (per knot, the reference's accumulation order)."""
+    N = len(X)
+    cost = 0.0
+    for t in range(N - 1):
+        dx, du = X[t] - Xref[t], U[t] - Uref[t]
+        cost += 0.5 * dx.T @ Q @ dx + 0.5 * du.T @ R @ du
+        hu = np.concatenate([U[t] - u_max, -U[t] + u_min])
+        cost += np.dot(mu[t], hu) + 0.5 * rho * hu.T @ _mask(mu[t], hu) @ hu
+        cost += np.dot(mux[t], hx[t]) + 0.5 * rho * hx[t].T @ _mask(mux[t], hx[t]) @ hx[t]
+    dx = X[-1] - Xref[-1]
+    cost += 0.5 * dx.T @ Qf @ dx
+    cost += np.dot(mux[-1], hx[-1]) + 0.5 * rho * hx[-1].T @ _mask(mux[-1], hx[-1]) @ hx[-1]
+    cost += np.dot(lam, dx) + 0.5 * rho * dx.T @ dx
+    return cost
+
+
+def stage_terms(Q, R, Qf, Xref, Uref, u_min, u_max, X, U, hx, Gx, mu, mux, lam, rho):
+    """Cost derivatives of backward_pass, ALTRO.py:254-300 -> (lx, lu, lxx, luu, VxT, VxxT)."""
+    N, nu = len(X), U.shape[1]
+    Gu = np.vstack([np.eye(nu), -np.eye(nu)])
+    lx, lu, lxx, luu = [], [], [], []
+    for t in range(N - 1):
+        hu = np.concatenate([U[t] - u_max, -U[t] + u_min])
+        mu_m, mx_m = _mask(mu[t], hu), _mask(mux[t], hx[t])
+        lx.append(Q @ (X[t] - Xref[t]) + Gx[t].T @ (mux[t] + rho * (mx_m @ hx[t])))
+        lu.append(R @ (U[t] - Uref[t]) + Gu.T @ (mu[t] + rho * (mu_m @ hu)))
+        lxx.append(Q + rho * Gx[t].T @ mx_m @ Gx[t])
+        luu.append(R + rho * Gu.T @ mu_m @ Gu)
+    g = X[-1] - Xref[-1]
+    m = _mask(mux[-1], hx[-1])
+    VxT = Qf @ g + Gx[-1].T @ (mux[-1] + rho * (m @ hx[-1])) + (lam + rho * g)
+    VxxT = Qf + rho * Gx[-1].T @ m @ Gx[-1] + rho * np.eye(len(g))
+    return np.array(lx), np.array(lu), np.array(lxx), np.array(luu), VxT, VxxT
+
+
+def victim_poses_piano(X):
+    """piano_mover.py:60-61: r = (x0, x1, 0), p = (0, 0, 1) tan(theta / 4)."""
+    return np.array([np.concatenate([[x[0], x[1], 0.0], np.array([0, 0, 1]) * np.tan(x[4] / 4)]) for x in X])
+
+
+def constraint_jacobian_piano(X, J):
+    """piano_mover.py:83-95 chain rule -> d(1 - alpha)/dx [N, ncx, 6]."""
+    out = []
+    for x, Jt in zip(X, J):
+        dp = np.array([0, 0, 1]) * (1 / (4 * np.cos(x[4] / 4) ** 2))
+        out.append([np.concatenate([-j[:2], [0, 0], [-np.dot(j[3:6], dp)], [0]]) for j in Jt])
+    return np.array(out)
+
+
+def constraint_jacobian_rigid(J):
+    """cluttered_hallway_quadrotor.py:159-168 / cone_through_wall.py:157-166."""
+    return np.array([[np.concatenate([-j[:3], np.zeros(3), -j[3:6], np.zeros(3)]) for j in Jt] for Jt in J])

@@ -262,3 +262,61 @@ def test_obstacle_field_matches_oracle(name):
     assert grad_close(J.reshape(-1, 12), Jw.reshape(-1, 12)).all()
     a2, none = gpu.evaluate(poses, False)
     assert none is None and np.array_equal(a2, a)
+
+
+# ------------------------------------------------------------------ AL objective pieces
+def _al_case(name, seed):
+    from altro import systems
+    rng = np.random.default_rng(seed)
+    params, X, U = systems.initialize(name)
+    N, nx, nu, nc = params["N"], params["nx"], params["nu"], len(params["P_obs"])
+    X = np.array(params["Xref"], dtype=float) + 0.3 * rng.normal(size=(N, nx))
+    U = np.array(U, dtype=float) + 0.5 * rng.normal(size=(N - 1, nu))
+    hx = rng.normal(size=(N, nc)) * 0.3
+    Gx = rng.normal(size=(N, nc, nx))
+    mu = np.maximum(0, rng.normal(size=(N - 1, 2 * nu)))
+    mux = np.maximum(0, rng.normal(size=(N, nc)))
+    lam = rng.normal(size=nx)
+    Uref = np.asarray(params["Uref"], dtype=float)[: N - 1]
+    args = (np.asarray(params["Q"], float), np.asarray(params["R"], float), np.asarray(params["Qf"], float),
+            np.asarray(params["Xref"], float), Uref, params["u_min"], params["u_max"])
+    return params, args, X, U, hx, Gx, mu, mux, lam
+
+
+@pytest.mark.parametrize("name", ["piano_mover", "coneThroughWall", "quadrotor"])
+def test_al_cost_and_stage_terms_match_reference_math(name):
+    from altro import _native
+    from oracle import altro_oracle as ao
+    params, args, X, U, hx, Gx, mu, mux, lam = _al_case(name, 11)
+    prob = _native.make_problem(params["N"], params["nx"], params["nu"], hx.shape[1], *args)
+    for rho in (1.0, 1e4):
+        J = _native.cost(prob, X, U, hx, mu, mux, lam, rho)
+        Jw = ao.al_cost(*args, X, U, hx, mu, mux, lam, rho)
+        assert abs(J - Jw) <= 1e-12 * abs(Jw)
+        got = _native.stage_terms(prob, X, U, hx, Gx, mu, mux, lam, rho)
+        want = ao.stage_terms(*args, X, U, hx, Gx, mu, mux, lam, rho)
+        for a, b in zip(got, want):
+            np.testing.assert_allclose(a, b, rtol=1e-12, atol=1e-12 * max(1.0, np.abs(b).max()))
+
+
+@pytest.mark.parametrize("name", ["piano_mover", "quadrotor"])
+def test_pose_map_and_constraint_jacobian(name):
+    from altro import _native, systems
+    from oracle import altro_oracle as ao
+    params, X, U = systems.initialize(name)
+    rng = np.random.default_rng(5)
+    X = np.array(params["Xref"], dtype=float) + 0.4 * rng.normal(size=(params["N"], params["nx"]))
+    J = rng.normal(size=(params["N"], len(params["P_obs"]), 12))
+    m = systems.get(name).native_model(params)
+    P = _native.victim_poses(m, X)
+    G = _native.constraint_jacobian(m, X, J)
+    if name == "piano_mover":
+        np.testing.assert_allclose(P, ao.victim_poses_piano(X), rtol=1e-15, atol=0)
+        np.testing.assert_allclose(G, ao.constraint_jacobian_piano(X, J), rtol=1e-14, atol=1e-15)
+    else:
+        np.testing.assert_array_equal(P, np.concatenate([X[:, :3], X[:, 6:9]], axis=1))
+        np.testing.assert_array_equal(G, ao.constraint_jacobian_rigid(J))
+    # the system module's NumPy forms (per-knot reference interface) agree too
+    mod = systems.get(name)
+    np.testing.assert_allclose(mod.victim_poses(params, X), P, rtol=1e-15, atol=0)
+    np.testing.assert_allclose(mod.state_jacobian(params, X, J), G, rtol=1e-14, atol=1e-15)
