@@ -7,6 +7,10 @@ per GPU, B = 100,000 (knot x primitive-pair) problems; primitives are rect-prism
 pair); poses r ~ U(-3, 3)^3, p (MRP) ~ U(-1, 1)^3; seed 0 (+ rank).  One "step" = one
 dcol_plan_run over the whole batch: conic assembly + PDIP (pdip_tol 1e-6) + the 12-gradient
 (FD mode = the reference's formulation) + alpha, with poses already resident in HBM.
+Steps are issued round-robin on --streams (default 2) HIP streams, each with its own output
+buffers, as a pipelined batch service would: the last, partly-filled round of one step's
+waves overlaps the first round of the next.  The one-stream (serialised) throughput is
+reported beside it (pipeline.serial_value), and kernel_ms is the per-launch duration.
 
 Multi-GPU: one process per GPU (torchrun); every rank solves its own 100k-pair shard
 (independent units, no data-path collective) -> "scaling": "weak"; the timed region is
@@ -109,6 +113,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check", type=int, default=256, help="pairs re-checked against the oracle")
     ap.add_argument("--max-iter", type=int, default=50, help="PDIP iteration cap (diagnostics only; reference: 50)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="steps are issued round-robin on this many HIP streams with their own output buffers "
+                         "(a pipelined batch service: one step's tail overlaps the next step's start)")
     ap.add_argument("--no-altro", action="store_true", help="skip the ALTRO wall-clock and scene-batch sections")
     ap.add_argument("--workload", choices=["poly100k", "mixed1m"], default="poly100k",
                     help="poly100k: BASELINE configs[3], 100k poly-poly pairs per GPU (weak scaling, the "
@@ -153,22 +160,31 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     step = plan.bind(pose1, pose2, out, grad=args.grad, contact=False, stream=stream, max_iter=args.max_iter)
+    # pipelined issue: S streams, each with its own outputs (poses are read-only, shared)
+    S = max(1, args.streams)
+    lanes = [step] + [plan.bind(pose1, pose2, alloc_outputs(B, dev, want_grad=True, want_contact=False),
+                                grad=args.grad, contact=False, stream=torch.cuda.Stream(dev), max_iter=args.max_iter)
+                      for _ in range(S - 1)]
 
-    for _ in range(args.warmup):
-        step()
+    for k in range(args.warmup):
+        lanes[k % S]()
     torch.cuda.synchronize(dev)
 
-    # the timed region: exactly K steps, barrier + synchronize on both sides, no events
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    def timed(fns):
+        """exactly K steps, barrier + synchronize on both sides, no events"""
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            fns[k % len(fns)]()
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        return time.perf_counter() - t0
+
+    elapsed_serial = timed([step]) if S > 1 else None
+    elapsed = timed(lanes)
 
     # kernel duration (roofline): HIP events on the launch stream, separate pass
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -179,9 +195,10 @@ def main():
     torch.cuda.synchronize(dev)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if dist is not None:
-        t = torch.tensor([elapsed, kern_ms], device=coll_dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, kern_ms, elapsed_serial or 0.0], device=coll_dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms_max = float(t[0]), float(t[1])
+        elapsed_serial = float(t[2]) if elapsed_serial is not None else None
     else:
         kern_ms_max = kern_ms
 
@@ -222,6 +239,10 @@ def main():
                           "peak": FP64_VECTOR_PEAK_TFS, "unit": "TFLOP/s",
                           "frac": flops_pair * B / (kern_ms * 1e-3) / 1e12 / FP64_VECTOR_PEAK_TFS,
                           "flops_per_pair": flops_pair},
+        "pipeline": {"streams": S, "note": "steps issued round-robin on S streams with separate outputs; "
+                     "value/ms_per_step are the pipelined throughput, serial_* the one-stream run",
+                     "serial_value": (B * world * args.steps / elapsed_serial) if elapsed_serial else value,
+                     "serial_ms_per_step": 1e3 * (elapsed_serial or elapsed) / args.steps},
         "kernel_ms": kern_ms,
         "kernel_ms_max_rank": kern_ms_max,
         "solve_stats": {"ok_frac": float(np.mean(status == 0)), "iters_mean": float(iters[status == 0].mean()),
