@@ -89,6 +89,7 @@ struct dcol_table {
 struct Launch {
     int kind;       // 0 = solve, 1 = reject
     int N, nsoc, omax, lpp;
+    bool full = false;   // every pair has o == omax: the padding-free kernel (DCOL_FULL_VARIANTS) if built
     int32_t code;   // reject status
     int64_t slot0, n;
     int lane = 0;   // 0 = caller's stream, 1..kSideStreams = table side stream
@@ -114,12 +115,12 @@ struct dcol_plan {
 
 namespace {
 
-hipError_t launch_variant(int N, int nsoc, int omax, int lpp, const KArgs& a, hipStream_t st) {
-    if (N == 4) return launch_n4(nsoc, omax, lpp, a, st);
-    if (N == 5) return launch_n5(nsoc, omax, lpp, a, st);
-    if (N == 6) return launch_n6(nsoc, omax, lpp, a, st);
-    if (N == 7) return launch_n7(nsoc, omax, lpp, a, st);
-    if (N == 8) return launch_n8(nsoc, omax, lpp, a, st);
+hipError_t launch_variant(int N, int nsoc, int omax, int lpp, bool full, const KArgs& a, hipStream_t st) {
+    if (N == 4) return launch_n4(nsoc, omax, lpp, full, a, st);
+    if (N == 5) return launch_n5(nsoc, omax, lpp, full, a, st);
+    if (N == 6) return launch_n6(nsoc, omax, lpp, full, a, st);
+    if (N == 7) return launch_n7(nsoc, omax, lpp, full, a, st);
+    if (N == 8) return launch_n8(nsoc, omax, lpp, full, a, st);
     return hipErrorInvalidValue;
 }
 
@@ -236,12 +237,15 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
     const int32_t ns = (int32_t)t->shapes.size();
     using Key = std::tuple<int, int, int, int, int, int>;   // kind, N, nsoc, omax, lpp, code
     std::map<Key, std::vector<int32_t>> groups;
+    std::map<Key, bool> full;
     for (int64_t i = 0; i < B; ++i) {
         if (s1[i] < 0 || s1[i] >= ns || s2[i] < 0 || s2[i] >= ns)
             return fail(DCOL_ERR_ARG, "shape id out of range at pair " + std::to_string(i));
         PairClass c = classify(t->shapes[s1[i]], t->shapes[s2[i]], case4);
         Key k = c.status == DCOL_OK ? Key{0, c.N, c.nsoc, c.omax, c.lpp, 0} : Key{1, 0, 0, 0, 0, c.status};
         groups[k].push_back((int32_t)i);
+        auto f = full.emplace(k, true).first;
+        f->second = f->second && c.o == c.omax;
     }
     p->table = t;
     p->B = B;
@@ -256,6 +260,7 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
         L.omax = std::get<3>(kv.first);
         L.lpp = std::get<4>(kv.first);
         L.code = std::get<5>(kv.first);
+        L.full = L.kind == 0 && full[kv.first];
         L.slot0 = (int64_t)perm.size();
         L.n = (int64_t)kv.second.size();
         if (L.kind == 0 && !lpp_forced() && L.n * L.lpp < 64LL * t->simds)   // cannot fill the GPU
@@ -428,7 +433,7 @@ int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, 
             hipLaunchKernelGGL(reject_kernel, dim3(grid), dim3(kBlock), 0, ls, a, L.code);
             e = hipGetLastError();
         } else {
-            e = launch_variant(L.N, L.nsoc, L.omax, L.lpp, a, ls);
+            e = launch_variant(L.N, L.nsoc, L.omax, L.lpp, L.full, a, ls);
         }
         if (e != hipSuccess) break;
     }

@@ -70,6 +70,15 @@ DCOL_HD double frsqrt(double x) {
 #endif
 }
 
+// x > 0 and finite (one v_cmp_class on the GPU: +subnormal | +normal)
+DCOL_HD bool pos_finite(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_class(x, 0x180);
+#else
+    return x > 0.0 && x < __builtin_inf();
+#endif
+}
+
 enum : int32_t { ST_OK = 0, ST_MAXITER = 1, ST_UNSUPPORTED = 2, ST_NOT_PD = 3, ST_NONFINITE = 4, ST_TOO_LARGE = 5 };
 enum : int32_t { SOC_NONE = 0, SOC_BALL = 1, SOC_CONE = 2 };
 enum : int32_t { F_GRAD_FD = 1, F_GRAD_ENV = 2, F_CONTACT = 4 };
@@ -419,7 +428,7 @@ struct Grp<4> {
 //    lambda\v = v/lambda share ONE reciprocal per row per iteration;
 //    lambda o lambda = s z;
 //  * the primal residual r = G x - h is carried incrementally (r += a G dx);
-//  * the orthant ratio test keeps the argmin by cross-multiplication and divides once;
+//  * orthant ratio tests as a running max of -d/x through the row reciprocals (bound_inv);
 //  * G~ = W^-1 G is never formed: G~'G~ and G~'v accumulate G'(W^-1 ...).
 template <int N, int NSOC, int OMAX, int LPP>
 struct Solver {
@@ -560,7 +569,10 @@ struct Solver {
         for (int j = 1; j < N; ++j) acc += G[k][j] * v[j];
         return acc;
     }
-    // upper Cholesky H = F'F (scipy.linalg.cholesky); false if a pivot is <= 0 or NaN
+    // upper Cholesky H = F'F (scipy.linalg.cholesky); false if a pivot is <= 0, infinite or
+    // NaN.  Any non-finite entry of H's upper triangle makes some pivot non-finite (a
+    // diagonal entry directly, an off-diagonal one through F[j][c]^2), so a non-finite H
+    // always fails here and the caller only classifies failures.
     DCOL_HD static bool chol(const double (&H)[N][N], double (&F)[N][N], double (&idg)[N]) {
         bool ok = true;
 #pragma unroll
@@ -568,7 +580,7 @@ struct Solver {
             double d = H[j][j];
 #pragma unroll
             for (int k = 0; k < j; ++k) d -= F[k][j] * F[k][j];
-            ok = ok && (d > 0.0);
+            ok = ok && pos_finite(d);
             idg[j] = frsqrt(d);
             F[j][j] = d * idg[j];
 #pragma unroll
@@ -694,15 +706,15 @@ struct Solver {
         return ok;
     }
 
-    // line-search candidate: keep argmin of x / (-d) over d < 0 by cross-multiplication
-    // Branch-free (selects, no exec-mask branches): the hot loop runs one of these per
-    // row bound per direction, and a divergent branch costs more than the compare.
-    DCOL_HD static void ratio(double xv, double d, bool valid, double& bn, double& bd) {
-        const double nd = -d;
-        const bool take = valid & (d < 0.0) & (xv * bd < bn * nd);
-        bn = take ? xv : bn;
-        bd = take ? nd : bd;
-    }
+    // Ratio tests in reciprocal form: the orthant step bound min(1, min_{d<0} x/(-d))
+    // (pdip.py:7-22) is 1 / max(1, max_i (-d_i / x_i)), accumulated as a running max of
+    // -d_i * (1/x_i) -- a multiply and a max per row bound instead of a compare-and-select
+    // argmin (the reciprocal 1/s is already at hand for every row).  Rows with d >= 0 give
+    // a candidate <= 0 and never win; inert padding rows (s = z = 1, G = 0, r = 0) give
+    // candidates -d <= 1 in both directions (ds = -1, dz = 0 or sigma mu), so no mask is
+    // needed.  Rounding-level only: the bound differs from the reference's quotient by a
+    // few ulp.
+    DCOL_HD static double bound_inv(double cmax, double d, double ix) { return fmax(cmax, -d * ix); }
 
     struct SocState {
         SocNT W;
@@ -711,15 +723,41 @@ struct Solver {
     };
 
     // -------- solve_lp_pdip, pdip.py:373-470 -------------------------------------------
+    // FULL: every orthant slot holds a real row (o == OMAX for the whole launch), so the
+    // padding masks of the loop fold away at compile time.
+    template <bool FULL>
+    DCOL_HD bool live(int k) const { return FULL || vort(k); }
+
+    template <bool FULL>
     DCOL_HD int32_t pdip(double tol, int max_iter, int* it_out) {
         int it = 0;
         int32_t st = ST_MAXITER;
         for (it = 0; it < max_iter; ++it) {
             DCOL_ISTAMP(it, 0);
-            // ---- NT scalings, residuals, normal matrix (pdip.py:410-434)
+            // ---- mu = s'z / deg and the exit test first (pdip.py:410-422, quirk Q3): the
+            // iteration that returns does not build the normal matrix
             double il[OR > 0 ? OR : 1];                 // orthant rows: 1 / s
+            double sz = 0.0;
+#pragma unroll
+            for (int k = 0; k < OR; ++k) {
+                il[k] = frcp(s[k]);
+                sz = fma(live<FULL>(k) ? s[k] : 0.0, z[k], sz);
+            }
+#pragma unroll
+            for (int b = 0; b < SS; ++b) {
+                const int k0 = OR + 4 * b;
+                const double szb = s[k0] * z[k0] + s[k0 + 1] * z[k0 + 1] + s[k0 + 2] * z[k0 + 2] + s[k0 + 3] * z[k0 + 3];
+                sz = vs[b] ? sz + szb : sz;
+            }
+            sz = R::sum(sz);
+            const double mu = sz / (double)deg;
+            if (mu < tol) {
+                st = ST_OK;
+                break;
+            }
+            // ---- NT scalings, residuals, normal matrix (pdip.py:410-434)
             SocState so[SSA];
-            double sz = 0.0, rx[N], Hm[N][N];
+            double rx[N], Hm[N][N];
 #pragma unroll
             for (int j = 0; j < N; ++j) {
                 rx[j] = 0.0;
@@ -728,9 +766,7 @@ struct Solver {
             }
 #pragma unroll
             for (int k = 0; k < OR; ++k) {
-                const double sk = s[k], zk = z[k];
-                il[k] = frcp(sk);
-                sz = fma(vort(k) ? sk : 0.0, zk, sz);
+                const double zk = z[k];
                 const double d = zk * il[k];              // W^-2 = z / s on the orthant
                 double g[N];
 #pragma unroll
@@ -749,8 +785,6 @@ struct Solver {
                 soc_nt(s + k0, z + k0, so[b].W);
                 soc_mul(so[b].W, z + k0, so[b].lam);
                 soc_prod(so[b].lam, so[b].lam, so[b].ll);
-                const double szb = s[k0] * z[k0] + s[k0 + 1] * z[k0 + 1] + s[k0 + 2] * z[k0 + 2] + s[k0 + 3] * z[k0 + 3];
-                sz = vs[b] ? sz + szb : sz;
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -777,51 +811,51 @@ struct Solver {
 #pragma unroll
                         for (int c = j; c < N; ++c) Hm[j][c] += gt[e][j] * gt[e][c];
             }
-            sz = R::sum(sz);
             allsum_vec(rx);
             allsum_sym(Hm);
             rx[3] += 1.0;                                   // + c (c = e_3)
             DCOL_ISTAMP(it, 1);
-            const double mu = sz / (double)deg;
-            if (mu < tol) {                                 // quirk Q3
-                st = ST_OK;
+            double F[N][N], idg[N];
+            if (!chol(Hm, F, idg)) {                        // scipy check_finite -> ValueError,
+                bool finite = true;                         // else LinAlgError (not PD)
+#pragma unroll
+                for (int j = 0; j < N; ++j)
+#pragma unroll
+                    for (int c = j; c < N; ++c) finite = finite && __builtin_isfinite(Hm[j][c]);
+                st = finite ? ST_NOT_PD : ST_NONFINITE;
                 break;
             }
-            bool finite = true;
-#pragma unroll
-            for (int j = 0; j < N; ++j)
-#pragma unroll
-                for (int c = j; c < N; ++c) finite = finite && __builtin_isfinite(Hm[j][c]);
-            if (!finite) { st = ST_NONFINITE; break; }       // scipy check_finite -> ValueError
-            double F[N][N], idg[N];
-            if (!chol(Hm, F, idg)) { st = ST_NOT_PD; break; }
             DCOL_ISTAMP(it, 2);
 
             // ---- predictor (affine) direction
-            double dsA[M], dzA[M];
+            double cp[M];                                // (W^-1 ds_a) o (W dz_a)
+            double dsS[SSA * 4], dzS[SSA * 4];           // SOC rows of the affine step
             double dx[N];
-            direction(so, il, F, idg, rx, nullptr, 0.0, dx, dsA, dzA);
-            double bn = 1.0, bd = 1.0, als = 1.0;
-            step_bound(so, dsA, dzA, bn, bd, als);
-            const double aa = R::min(fmin(bn / bd, als));           // quirk Q5 (no 0.99)
+            double cmax = 1.0, als = 1.0, p1 = 0.0, p2 = 0.0;
+            predictor<FULL>(so, il, F, idg, rx, dx, cp, dsS, dzS, cmax, p1, p2);
+            soc_bound(dsS, dzS, als);
+            const double aa = R::min(fmin(frcp(cmax), als));        // quirk Q5 (no 0.99)
             DCOL_ISTAMP(it, 3);
-            double rho = 0.0;
+            // rho = (s + aa ds)'(z + aa dz) / s'z, expanded as
+            // s'z + aa (s'dz + z'ds) + aa^2 ds'dz (orthant sums accumulated by predictor())
 #pragma unroll
-            for (int k = 0; k < M; ++k)
-                rho = fma(vrow(k) ? s[k] + aa * dsA[k] : 0.0, z[k] + aa * dzA[k], rho);
-            rho = R::sum(rho) * frcp(sz);
+            for (int b = 0; b < SS; ++b)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int k = OR + 4 * b + e;
+                    const double dsk = dsS[4 * b + e], dzk = dzS[4 * b + e];
+                    p1 = vs[b] ? fma(s[k], dzk, fma(z[k], dsk, p1)) : p1;
+                    p2 = vs[b] ? fma(dsk, dzk, p2) : p2;
+                }
+            const double rho = (sz + R::sum(fma(aa, p1, (aa * aa) * p2))) * frcp(sz);
             const double sc = fmax(0.0, fmin(1.0, rho));
             const double sigma = sc * sc * sc;                      // quirk Q6
-            // cp = (W^-1 ds_a) o (W dz_a)
-            double cp[M];
-#pragma unroll
-            for (int k = 0; k < OR; ++k) cp[k] = dsA[k] * dzA[k];     // (W^-1 ds_a) o (W dz_a), orthant
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
                 const int k0 = OR + 4 * b;
                 double t1[4], t2[4];
-                soc_solve(so[b].W, dsA + k0, t1);
-                soc_mul(so[b].W, dzA + k0, t2);
+                soc_solve(so[b].W, dsS + 4 * b, t1);
+                soc_mul(so[b].W, dzS + 4 * b, t2);
                 soc_prod(t1, t2, cp + k0);
             }
 
@@ -832,13 +866,13 @@ struct Solver {
             DCOL_ISTAMP(it, 4);
             rhs_solve(so, il, F, idg, rx, cp, smu, dx, sbzt, slds);
             DCOL_ISTAMP(it, 5);
-            bn = 1.0; bd = 1.0; als = 1.0;
+            cmax = 1.0; als = 1.0;
 #pragma unroll
             for (int k = 0; k < OR; ++k) {
                 double u, dzk, dsk;
                 orth_step(k, il, cp, smu, dx, u, dzk, dsk);
-                ratio(s[k], dsk, vort(k), bn, bd);
-                ratio(z[k], dzk, vort(k), bn, bd);
+                cmax = bound_inv(cmax, dsk, il[k]);
+                cmax = bound_inv(cmax, dzk, frcp(z[k]));
             }
             double sdz[SSA][4], sds[SSA][4], su[SSA][4];
 #pragma unroll
@@ -848,7 +882,7 @@ struct Solver {
                 const double lb = fmin(soc_ls(s + k0, sds[b]), soc_ls(z + k0, sdz[b]));
                 als = vs[b] ? fmin(als, lb) : als;
             }
-            const double a = fmin(1.0, 0.99 * R::min(fmin(bn / bd, als)));
+            const double a = fmin(1.0, 0.99 * R::min(fmin(frcp(cmax), als)));
             DCOL_ISTAMP(it, 6);
 #pragma unroll
             for (int j = 0; j < N; ++j) x[j] += a * dx[j];
@@ -857,7 +891,7 @@ struct Solver {
                 double u, dzk, dsk;
                 orth_step(k, il, cp, smu, dx, u, dzk, dsk);
                 r[k] += a * u;
-                const bool v = vort(k);
+                const bool v = live<FULL>(k);
                 s[k] = v ? s[k] + a * dsk : s[k];
                 z[k] = v ? z[k] + a * dzk : z[k];
             }
@@ -940,20 +974,34 @@ struct Solver {
         }
         (void)lds;
     }
-    // full direction with stored ds/dz (predictor: they feed rho and the corrector's cp)
-    DCOL_HD void direction(const SocState* so, const double* il, const double (&F)[N][N], const double (&idg)[N],
-                           const double* rx, const double* cp, double smu, double* dx, double* ds, double* dz) const {
+    // predictor (affine) direction and the orthant part of its step bound.  Orthant rows:
+    // dz = z t with t = (u + r) / s, so the z-row bound candidate -dz/z is -t itself; their
+    // ds/dz are not kept -- only cp = ds o dz (the corrector's cross term) and the sums
+    // p1 = s'dz + z'ds, p2 = ds'dz that rho needs.  SOC rows keep ds/dz (dsS, dzS).
+    template <bool FULL>
+    DCOL_HD void predictor(const SocState* so, const double* il, const double (&F)[N][N], const double (&idg)[N],
+                           const double* rx, double* dx, double* cp, double* dsS, double* dzS, double& cmax,
+                           double& p1, double& p2) const {
         double sbzt[SSA][4], slds[SSA][4];
-        rhs_solve(so, il, F, idg, rx, cp, smu, dx, sbzt, slds);
+        rhs_solve(so, il, F, idg, rx, nullptr, 0.0, dx, sbzt, slds);
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
-            double u;
-            orth_step(k, il, cp, smu, dx, u, dz[k], ds[k]);
+            const double u = rowdot(k, dx);
+            const double t = (u + r[k]) * il[k];
+            const double dz = z[k] * t;
+            const double ds = -(s[k] + r[k]) - u;
+            cmax = bound_inv(cmax, ds, il[k]);
+            cmax = fmax(cmax, -t);
+            const double c = ds * dz;
+            cp[k] = c;
+            const bool v = live<FULL>(k);
+            p1 = v ? fma(s[k], dz, fma(z[k], ds, p1)) : p1;
+            p2 = v ? p2 + c : p2;
         }
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
             double u[4];
-            soc_step(so[b], OR + 4 * b, sbzt[b], slds[b], dx, u, dz + OR + 4 * b, ds + OR + 4 * b);
+            soc_step(so[b], OR + 4 * b, sbzt[b], slds[b], dx, u, dzS + 4 * b, dsS + 4 * b);
         }
     }
     // z v + (smu - cp) on the corrector, z v on the predictor
@@ -972,21 +1020,15 @@ struct Solver {
         if (cp) v[0] += smu;
         soc_iprod(S.lam, v, out);
     }
-    // ratio tests of s + a ds >= 0, z + a dz >= 0 over the lane's rows
-    DCOL_HD void step_bound(const SocState* so, const double* ds, const double* dz, double& bn, double& bd,
-                            double& als) const {
-#pragma unroll
-        for (int k = 0; k < OR; ++k) {
-            ratio(s[k], ds[k], vort(k), bn, bd);
-            ratio(z[k], dz[k], vort(k), bn, bd);
-        }
+    // SOC part of the step bound (soc_linesearch over the lane's blocks; ds/dz hold the
+    // SOC rows only)
+    DCOL_HD void soc_bound(const double* ds, const double* dz, double& als) const {
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
             const int k0 = OR + 4 * b;
-            const double lb = fmin(soc_ls(s + k0, ds + k0), soc_ls(z + k0, dz + k0));
+            const double lb = fmin(soc_ls(s + k0, ds + 4 * b), soc_ls(z + k0, dz + 4 * b));
             als = vs[b] ? fmin(als, lb) : als;
         }
-        (void)so;
     }
 
     // -------- gradient helpers ---------------------------------------------------------
@@ -1190,7 +1232,9 @@ DCOL_HD void launder(P& p) {
 #endif
 }
 
-template <int N, int NSOC, int OMAX, int LPP>
+// FULL: every pair of the launch has o == OMAX (no padding rows; the host picks the
+// variant per launch, dcol_capi.cpp: bucket_pairs)
+template <int N, int NSOC, int OMAX, int LPP, bool FULL = false>
 DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
     DCOL_STAMP(A, pi, q, 0);
     const int64_t B = A.B;
@@ -1220,7 +1264,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
     const bool init_ok = P.initialize();
     DCOL_STAMP(A, pi, q, 3);
     if (!init_ok) st = ST_NOT_PD;
-    else st = P.pdip(A.tol, A.max_iter, &it);
+    else st = P.template pdip<FULL>(A.tol, A.max_iter, &it);
     DCOL_STAMP(A, pi, q, 4);
 
     const double nan = __builtin_nan("");
@@ -1281,14 +1325,14 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
 constexpr int kSolveBlock = DCOL_BLOCK;
 static_assert(kSolveBlock % 64 == 0, "one or more whole waves per workgroup");
 
-template <int N, int NSOC, int OMAX, int LPP, int WPS>
+template <int N, int NSOC, int OMAX, int LPP, int WPS, bool FULL>
 __global__ void __launch_bounds__(kSolveBlock, WPS) prox_kernel(KArgs A) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t slot = t / LPP;
     const int q = (int)(t % LPP);
     if (slot >= A.n) return;
     const int64_t pi = A.perm ? (int64_t)A.perm[A.slot0 + slot] : (A.slot0 + slot);
-    solve_one<N, NSOC, OMAX, LPP>(A, pi, q);
+    solve_one<N, NSOC, OMAX, LPP, FULL>(A, pi, q);
 }
 
 }  // namespace dcol

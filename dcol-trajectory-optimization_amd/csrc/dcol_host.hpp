@@ -45,7 +45,7 @@ inline const std::map<std::pair<int, int>, std::vector<int>>& buckets() {
 // mostly idle)
 inline int max_lpp(int N, int nsoc, int omax) {
     int best = 0;
-#define DCOL_MAXL(NN, NS, OM, LP, WP) \
+#define DCOL_MAXL(NN, NS, OM, LP, WP, FL) \
     if (NN == N && NS == nsoc && OM == omax && LP > best) best = LP;
     DCOL_VARIANTS(DCOL_MAXL)
 #undef DCOL_MAXL
@@ -58,7 +58,7 @@ inline int choose_lpp(int N, int nsoc, int omax) {
         return e ? std::atoi(e) : 0;
     }();
     int first = 0;
-#define DCOL_PICK(NN, NS, OM, LP, WP)                              \
+#define DCOL_PICK(NN, NS, OM, LP, WP, FL)                          \
     if (NN == N && NS == nsoc && OM == omax) {                     \
         if (first == 0) first = LP;                                \
         if (forced == LP) return LP;                               \

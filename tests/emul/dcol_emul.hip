@@ -55,8 +55,18 @@ extern "C" int dcol_emul_batch(const dcol_shape_desc* shapes, int32_t n, int64_t
             for (int q = 0; q < 12; ++q) gr[q * B + i] = __builtin_nan("");
             continue;
         }
-#define DCOL_EMUL(NN, NS, OM) \
-        if (c.N == NN && c.nsoc == NS && c.omax == OM) { solve_one<NN, NS, OM, 1>(A, i, 0); continue; }
+        const bool full = c.o == c.omax;   // both loop specialisations, as the GPU launches pick them
+#define DCOL_EMUL(NN, NS, OM)                                                    \
+        if (c.N == NN && c.nsoc == NS && c.omax == OM) {                         \
+            if constexpr (NN == 4 && NS == 0) {   /* variants.py FULL shapes */  \
+                if (full) {                                                      \
+                    solve_one<NN, NS, OM, 1, true>(A, i, 0);                     \
+                    continue;                                                    \
+                }                                                                \
+            }                                                                    \
+            solve_one<NN, NS, OM, 1, false>(A, i, 0);                            \
+            continue;                                                            \
+        }
         DCOL_SHAPES(DCOL_EMUL)
 #undef DCOL_EMUL
         return fail(DCOL_ERR_ARG, "no variant");

@@ -25,7 +25,7 @@ __global__ void __launch_bounds__(64, {w}) kb(KArgs A) {{
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t slot = t / LP; const int q = (int)(t % LP);
     if (slot >= A.n) return;
-    solve_one<N, NS, OM, LP>(A, slot, q);
+    solve_one<N, NS, OM, LP, false>(A, slot, q);
 }}
 template __global__ void kb<{n},{s},{o},{l}>(KArgs); }}
 """
