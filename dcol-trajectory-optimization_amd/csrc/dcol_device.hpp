@@ -90,7 +90,8 @@ struct DevShape {
     int32_t row_off;   // first row in the row pool
     int32_t soc_kind;  // SOC_NONE / SOC_BALL / SOC_CONE
     int32_t n_extra;   // extra primal columns (capsule/cylinder 1, polygon 2)
-    int32_t pad0, pad1, pad2;
+    int32_t plain;     // r_off == 0 and Q_off == I (make_frame skips the offset products)
+    int32_t pad1, pad2;
     double R;          // ball SOC radius (sphere/capsule/cylinder/polygon)
     double cone_c;     // cone SOC row 0, column 3: -(tan(beta) * 3 * H / 4)
     double tanb;       // cone: tan(beta)  (E = diag(tanb, 1, 1))
@@ -190,21 +191,35 @@ DCOL_HD void dcm_from_mrp(double p1, double p2, double p3, double Q[9]) {
     Q[8] = (-((8.0 * (p1 * p1) + 8.0 * (p2 * p2)) * iden - 1.0) * den) * iden;
 }
 
-// problem_matrices.py:275-282 (r_eff = r + Q r_offset; Q_eff = Q Q_offset)
+// problem_matrices.py:275-282 (r_eff = r + Q r_offset; Q_eff = Q Q_offset).  With
+// identity offsets (S.plain) the products are exact no-ops (q*1 + q'*0 + q''*0 == q,
+// r + (+-0) == r) and are skipped: same bits, ~36 fewer instructions per frame.
 DCOL_HD void make_frame(const DevShape& S, const double th[6], Frame& F) {
     double Q[9];
     dcm_from_mrp(th[3], th[4], th[5], Q);
-    const double o0 = S.r_off[0], o1 = S.r_off[1], o2 = S.r_off[2];
+    double qe[9], qr[3];
+    if (S.plain) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        F.qro[k] = Q[3 * k] * o0 + Q[3 * k + 1] * o1 + Q[3 * k + 2] * o2;
-        F.re[k] = th[k] + F.qro[k];
+        for (int k = 0; k < 9; ++k) qe[k] = Q[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) qr[k] = 0.0;
+    } else {
+        const double o0 = S.r_off[0], o1 = S.r_off[1], o2 = S.r_off[2];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) qr[k] = Q[3 * k] * o0 + Q[3 * k + 1] * o1 + Q[3 * k + 2] * o2;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                qe[3 * r + c] = Q[3 * r] * S.Q_off[c] + Q[3 * r + 1] * S.Q_off[3 + c] + Q[3 * r + 2] * S.Q_off[6 + c];
     }
 #pragma unroll
-    for (int r = 0; r < 3; ++r)
+    for (int k = 0; k < 9; ++k) F.Qe[k] = qe[k];
 #pragma unroll
-        for (int c = 0; c < 3; ++c)
-            F.Qe[3 * r + c] = Q[3 * r] * S.Q_off[c] + Q[3 * r + 1] * S.Q_off[3 + c] + Q[3 * r + 2] * S.Q_off[6 + c];
+    for (int k = 0; k < 3; ++k) {
+        F.qro[k] = qr[k];
+        F.re[k] = th[k] + qr[k];
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -736,11 +751,13 @@ struct Solver {
             DCOL_ISTAMP(it, 0);
             // ---- mu = s'z / deg and the exit test first (pdip.py:410-422, quirk Q3): the
             // iteration that returns does not build the normal matrix
-            double il[OR > 0 ? OR : 1];                 // orthant rows: 1 / s
+            double il[OR > 0 ? OR : 1], iz[OR > 0 ? OR : 1];   // orthant rows: 1 / s, 1 / z
             double sz = 0.0;
 #pragma unroll
             for (int k = 0; k < OR; ++k) {
-                il[k] = frcp(s[k]);
+                const double rsz = frcp(s[k] * z[k]);   // one reciprocal for both
+                il[k] = z[k] * rsz;
+                iz[k] = s[k] * rsz;
                 sz = fma(live<FULL>(k) ? s[k] : 0.0, z[k], sz);
             }
 #pragma unroll
@@ -811,9 +828,8 @@ struct Solver {
 #pragma unroll
                         for (int c = j; c < N; ++c) Hm[j][c] += gt[e][j] * gt[e][c];
             }
-            allsum_vec(rx);
-            allsum_sym(Hm);
-            rx[3] += 1.0;                                   // + c (c = e_3)
+            allsum_sym(Hm);                                 // rx stays lane-partial: it is reduced
+                                                            // inside each right-hand side
             DCOL_ISTAMP(it, 1);
             double F[N][N], idg[N];
             if (!chol(Hm, F, idg)) {                        // scipy check_finite -> ValueError,
@@ -859,20 +875,21 @@ struct Solver {
                 soc_prod(t1, t2, cp + k0);
             }
 
-            // ---- corrector (combined) direction.  ds/dz/G dx are consumed by the ratio
-            // test as they are produced and recomputed in the update (register budget).
+            // ---- corrector (combined) direction; orthant G dx and dz are kept for the
+            // update, ds (two adds) is recomputed there.
             const double smu = sigma * mu;
             double sbzt[SSA][4], slds[SSA][4];
             DCOL_ISTAMP(it, 4);
             rhs_solve(so, il, F, idg, rx, cp, smu, dx, sbzt, slds);
             DCOL_ISTAMP(it, 5);
             cmax = 1.0; als = 1.0;
+            double cu[OR > 0 ? OR : 1], cdz[OR > 0 ? OR : 1];   // G dx and dz, kept for the update
 #pragma unroll
             for (int k = 0; k < OR; ++k) {
-                double u, dzk, dsk;
-                orth_step(k, il, cp, smu, dx, u, dzk, dsk);
+                double dsk;
+                orth_step(k, il, cp, smu, dx, cu[k], cdz[k], dsk);
                 cmax = bound_inv(cmax, dsk, il[k]);
-                cmax = bound_inv(cmax, dzk, frcp(z[k]));
+                cmax = bound_inv(cmax, cdz[k], iz[k]);
             }
             double sdz[SSA][4], sds[SSA][4], su[SSA][4];
 #pragma unroll
@@ -888,12 +905,11 @@ struct Solver {
             for (int j = 0; j < N; ++j) x[j] += a * dx[j];
 #pragma unroll
             for (int k = 0; k < OR; ++k) {
-                double u, dzk, dsk;
-                orth_step(k, il, cp, smu, dx, u, dzk, dsk);
-                r[k] += a * u;
+                const double dsk = -(s[k] + r[k]) - cu[k];
+                r[k] += a * cu[k];
                 const bool v = live<FULL>(k);
                 s[k] = v ? s[k] + a * dsk : s[k];
-                z[k] = v ? z[k] + a * dzk : z[k];
+                z[k] = v ? z[k] + a * cdz[k] : z[k];
             }
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
@@ -944,9 +960,10 @@ struct Solver {
 #pragma unroll
                 for (int j = 0; j < N; ++j) rhs[j] += G[k0 + e][j] * sbzt[b][e];
         }
-        allsum_vec(rhs);
 #pragma unroll
-        for (int j = 0; j < N; ++j) rhs[j] -= rx[j];
+        for (int j = 0; j < N; ++j) rhs[j] -= rx[j];     // lane partials of G'z
+        allsum_vec(rhs);
+        rhs[3] -= 1.0;                                   // - c (c = e_3)
         chol_solve(F, idg, rhs, dx);
     }
     // One orthant row of the step.  With W = diag(sqrt(s/z)) and lambda = W z the
@@ -1108,20 +1125,20 @@ struct Solver {
 
     // scipy approx_fprime(theta, f, sqrt(eps)) restricted to primitive prim's 6 coordinates
     // (proximity_gradient.py:50-88): forward differences of f_k with the reference's step
-    // rule, f_k evaluated through lag_aggregate / lag_pose_part.  Translation perturbations
-    // keep the rotation (only r_eff moves).
-    DCOL_HD void fd_grad_prim(const KArgs& A, const DevShape& S, int prim, const double th0[6], double* g) const {
+    // rule, f_k evaluated through lag_pose_part on the aggregate ag (lag_aggregate, group
+    // sums already taken).  Translation perturbations keep the rotation (only r_eff moves).
+    // The quotient uses the reciprocal of the exact step dx_j (rounding-level).
+    DCOL_HD void fd_grad_prim(const LagAgg& ag, const DevShape& S, int prim, const double th0[6], double* g) const {
         const double hstep = 1.4901161193847656e-08;   // sqrt(finfo(float).eps)
-        double tj[6], dxj[6];
+        double tj[6], idx[6];
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
             double hj = hstep;
             if ((th0[j] + hstep) - th0[j] == 0.0)       // _numdiff: fall back to a relative step
                 hj = hstep * (th0[j] >= 0.0 ? 1.0 : -1.0) * fmax(1.0, fabs(th0[j]));
             tj[j] = th0[j] + hj;
-            dxj[j] = tj[j] - th0[j];
+            idx[j] = frcp(tj[j] - th0[j]);
         }
-        const LagAgg ag = lag_aggregate(A, S, prim);
         Frame F0;
         make_frame(S, th0, F0);
         const double f0 = lag_pose_part(ag, S, prim, F0);
@@ -1130,7 +1147,7 @@ struct Solver {
             Frame Fj = F0;
 #pragma unroll
             for (int c = 0; c < 3; ++c) Fj.re[c] = (c == j ? tj[j] : th0[c]) + F0.qro[c];
-            g[j] = (lag_pose_part(ag, S, prim, Fj) - f0) / dxj[j];
+            g[j] = (lag_pose_part(ag, S, prim, Fj) - f0) * idx[j];
         }
 #pragma unroll
         for (int j = 3; j < 6; ++j) {
@@ -1139,7 +1156,7 @@ struct Solver {
             for (int c = 0; c < 6; ++c) th[c] = (c == j) ? tj[j] : th0[c];
             Frame Fj;
             make_frame(S, th, Fj);
-            g[j] = (lag_pose_part(ag, S, prim, Fj) - f0) / dxj[j];
+            g[j] = (lag_pose_part(ag, S, prim, Fj) - f0) * idx[j];
         }
     }
 
@@ -1147,40 +1164,16 @@ struct Solver {
     //   d/dr = zeta - Qe w;  d/dp_j = d' Q_j (Qoff w) - (Qe w - zeta)' Q_j r_off + zeta' Q_j (Qoff xi)
     // w = sum z_i a_i over rotated rows (body frame), zeta = z of the ball SOC rows 1..3,
     // xi = (x4, x5, 0) on the extra columns, d = x[0:3] - r_eff
-    DCOL_HD void env_grad_prim(const KArgs& A, const DevShape& S, int prim, const double th[6], double* g) const {
+    DCOL_HD void env_grad_prim(const LagAgg& ag, const DevShape& S, int prim, const double th[6], double* g) const {
         Frame Fr;
         make_frame(S, th, Fr);
-        const double* __restrict__ rows = reinterpret_cast<const double*>(A.rows);
-        double w[3] = {0.0, 0.0, 0.0}, zeta[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-        for (int k = 0; k < OR; ++k) {
-            if (owns_row(k, prim)) {
-                const int i = k * LPP + q;
-                const int ri = S.row_off + ((prim == 0) ? i : (i - o1));
-                const double2* rw = reinterpret_cast<const double2*>(rows + 8 * (int64_t)ri);
-                const double2 q0 = rw[0], q1 = rw[1];
-                w[0] += z[k] * q0.x;
-                w[1] += z[k] * q0.y;
-                w[2] += z[k] * q1.x;
-            }
-        }
-#pragma unroll
-        for (int b = 0; b < SS; ++b) {
-            if (vs[b] && soc_owner[b] == prim) {
-                const double* zb = z + OR + 4 * b;
-                if (S.soc_kind == SOC_CONE) {
-                    w[0] -= zb[0] * S.tanb;     // a_k = -E_kk e_k
-                    w[1] -= zb[1];
-                    w[2] -= zb[2];
-                } else {
-                    zeta[0] = zb[1]; zeta[1] = zb[2]; zeta[2] = zb[3];
-                }
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            w[c] = R::sum(w[c]);
-            zeta[c] = R::sum(zeta[c]);
+        double w[3] = {ag.w[0], ag.w[1], ag.w[2]}, zeta[3] = {0.0, 0.0, 0.0};
+        if (ag.kind == SOC_CONE) {          // a_k = -E_kk e_k
+            w[0] -= ag.zs[0] * S.tanb;
+            w[1] -= ag.zs[1];
+            w[2] -= ag.zs[2];
+        } else if (ag.kind == SOC_BALL) {
+            zeta[0] = ag.zs[1]; zeta[1] = ag.zs[2]; zeta[2] = ag.zs[3];
         }
         double xi[3] = {0.0, 0.0, 0.0};
         if (S.soc_kind == SOC_BALL) {
@@ -1289,12 +1282,30 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
         const DevShape& T1 = L.shapes[k1];
         const DevShape& T2 = L.shapes[k2];
         if (ok) {
-            if (A.flags & F_GRAD_ENV) {
-                P.env_grad_prim(L, T1, 0, th1, g);
-                P.env_grad_prim(L, T2, 1, th2, g + 6);
-            } else {
-                P.fd_grad_prim(L, T1, 0, th1, g);
-                P.fd_grad_prim(L, T2, 1, th2, g + 6);
+            // group sums for both primitives first (every lane of the group), then each
+            // lane differentiates one primitive: lane q takes primitive q & 1, so a 2+-lane
+            // group does the two 6-coordinate gradients side by side instead of both in
+            // every lane (a 1-lane group does both in turn)
+            using Agg = typename Solver<N, NSOC, OMAX, LPP>::LagAgg;
+            const Agg ag0 = P.lag_aggregate(L, T1, 0);
+            const Agg ag1 = P.lag_aggregate(L, T2, 1);
+            constexpr int NP = LPP >= 2 ? 1 : 2;
+#pragma unroll
+            for (int pp = 0; pp < NP; ++pp) {
+                const int prim = LPP >= 2 ? (q & 1) : pp;
+                const DevShape& T = prim ? T2 : T1;
+                Agg ag;   // element-wise select (a reference select would put both on the stack)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) ag.w[c] = prim ? ag1.w[c] : ag0.w[c];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) ag.zs[c] = prim ? ag1.zs[c] : ag0.zs[c];
+                ag.kind = prim ? ag1.kind : ag0.kind;
+                double th[6];
+#pragma unroll
+                for (int c = 0; c < 6; ++c) th[c] = prim ? th2[c] : th1[c];
+                double* gp = g + 6 * pp;
+                if (A.flags & F_GRAD_ENV) P.env_grad_prim(ag, T, prim, th, gp);
+                else P.fd_grad_prim(ag, T, prim, th, gp);
             }
         } else {
 #pragma unroll
@@ -1302,6 +1313,17 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
         }
     }
     DCOL_STAMP(A, pi, q, 5);
+    if (want_grad) {
+        if (LPP >= 2) {   // lane 1 of the group holds primitive 2's block (see above)
+            if (q == 1) {
+#pragma unroll
+                for (int c = 0; c < 6; ++c) A.grad[(6 + c) * B + pi] = ok ? g[c] : nan;
+            }
+        } else {
+#pragma unroll
+            for (int c = 6; c < 12; ++c) A.grad[c * B + pi] = g[c];
+        }
+    }
     if (q != 0) return;
     A.alpha[pi] = ok ? P.x[3] : nan;
     if (A.iters) A.iters[pi] = it;
@@ -1312,7 +1334,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
     }
     if (want_grad) {
 #pragma unroll
-        for (int c = 0; c < 12; ++c) A.grad[c * B + pi] = g[c];
+        for (int c = 0; c < 6; ++c) A.grad[c * B + pi] = g[c];
     }
 }
 

@@ -77,6 +77,12 @@ inline int digest_shape(const dcol_shape_desc& d, int32_t idx, DevShape& S, std:
     S.row_off = (int32_t)rows.size();
     for (int k = 0; k < 3; ++k) S.r_off[k] = d.r_offset[k];
     for (int k = 0; k < 9; ++k) S.Q_off[k] = d.Q_offset[k];
+    {   // identity offsets: make_frame's products with them are exact no-ops and are skipped
+        bool plain = true;
+        for (int k = 0; k < 3; ++k) plain = plain && S.r_off[k] == 0.0;
+        for (int k = 0; k < 9; ++k) plain = plain && S.Q_off[k] == ((k % 4 == 0) ? 1.0 : 0.0);
+        S.plain = plain ? 1 : 0;
+    }
     auto add = [&](double a0, double a1, double a2, double g3, double e0, double e1) {
         DevRow r;
         std::memset(&r, 0, sizeof(r));
