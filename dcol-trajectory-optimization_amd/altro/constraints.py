@@ -13,12 +13,14 @@ and solves a phase with one dcol_plan_run:
 
 Alpha-only phases (line-search trials) launch without the gradient flag.  The gradient
 solve also returns alpha, which the driver reuses for the cost of the same trajectory.
+The outputs live in ONE device buffer [alpha | status, iters | grad] mirrored by one pinned
+host buffer, so a phase is one H2D copy, one (fused) launch and one D2H copy.
 """
 from __future__ import annotations
 
 import numpy as np
 
-from dcol_amd.engine import DEFAULT_TOL, PDIPFailure, alloc_outputs, default_engine, raise_for_status
+from dcol_amd.engine import DEFAULT_TOL, PDIPFailure, default_engine, raise_for_status
 from dcol_amd.shapes import pose_of
 
 
@@ -40,19 +42,27 @@ class ObstacleField:
         obs_pose = np.array([pose_of(o) for o in obstacles], dtype=np.float64).reshape(self.n_obs, 6)
         self.pose2 = torch.from_numpy(np.ascontiguousarray(np.tile(obs_pose, (self.N, 1)).T)).to(dev)
         self.pose1 = torch.empty((6, B), dtype=torch.float64, device=dev)
-        self.out = alloc_outputs(B, dev, want_grad=True, want_contact=False)
+        # packed outputs: [alpha B | status B int32, iters B int32 | grad 12 x B] (float64 slots)
+        self.d_out = torch.empty(14 * B, dtype=torch.float64, device=dev)
+        self.out = self._views(self.d_out, B)
         self.stream = torch.cuda.current_stream(dev)
         self._launch = {True: self.plan.bind(self.pose1, self.pose2, self.out, tol=tol, grad=grad, stream=self.stream),
                         False: self.plan.bind(self.pose1, self.pose2, self.out, tol=tol, grad=None,
                                               stream=self.stream)}
         pin = dict(pin_memory=True)
         self.h_pose1 = torch.empty((6, B), dtype=torch.float64, **pin)
-        self.h_alpha = torch.empty(B, dtype=torch.float64, **pin)
-        self.h_grad = torch.empty((12, B), dtype=torch.float64, **pin)
-        self.h_status = torch.empty(B, dtype=torch.int32, **pin)
+        self.h_out = torch.empty(14 * B, dtype=torch.float64, **pin)
+        h = self._views(self.h_out, B)
+        self.h_alpha, self.h_status, self.h_grad = h["alpha"], h["status"], h["grad"]
         self.batches = 0
         self.pairs = 0
         self._warm(pose_of(victim))
+
+    @staticmethod
+    def _views(flat, B):
+        import torch
+        ints = flat[B:2 * B].view(torch.int32)
+        return {"alpha": flat[:B], "status": ints[:B], "iters": ints[B:2 * B], "grad": flat[2 * B:].view(12, B)}
 
     def _warm(self, pose):
         """Launch both variants once (loads the code objects; outputs discarded)."""
@@ -71,10 +81,8 @@ class ObstacleField:
         hp[:] = np.repeat(P.T, self.n_obs, axis=1)
         self.pose1.copy_(self.h_pose1, non_blocking=True)
         self._launch[bool(grad)]()
-        self.h_alpha.copy_(self.out["alpha"], non_blocking=True)
-        self.h_status.copy_(self.out["status"], non_blocking=True)
-        if grad:
-            self.h_grad.copy_(self.out["grad"], non_blocking=True)
+        n = 14 * self.B if grad else 2 * self.B      # alpha-only phases skip the gradient block
+        self.h_out[:n].copy_(self.d_out[:n], non_blocking=True)
         self.stream.synchronize()
         self.batches += 1
         self.pairs += self.B

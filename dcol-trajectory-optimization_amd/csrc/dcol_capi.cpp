@@ -7,7 +7,8 @@
 //  * dcol_plan_create: classifies each pair (combine_problem_matrices.py:3-70 cases 1-3 vs
 //    the unsupported case 4) and buckets pairs by kernel variant (N, NSOC, OMAX).
 //  * dcol_plan_run: one kernel launch per non-empty bucket, asynchronous on the caller's
-//    stream, no allocation (graph-capturable).
+//    stream, no allocation (graph-capturable) -- or, for a small plan that mixes variants,
+//    ONE fused launch covering every bucket (dcol_kernels_fused.hip).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -106,6 +107,11 @@ struct dcol_plan {
     int lanes = 1;               // streams the launches are spread over (1 = serial)
     hipEvent_t fork = nullptr;   // recorded on the caller's stream, awaited by the side streams
     hipEvent_t join[kSideStreams] = {};
+    // fused launch (small mixed plans): one segment per solve bucket, in launch order
+    std::vector<FusedSeg> segs;
+    FusedSeg* d_segs = nullptr;
+    int64_t fused_blocks = 0;
+    bool fused() const { return !segs.empty(); }
     ~dcol_plan() {
         if (fork) (void)hipEventDestroy(fork);
         for (hipEvent_t& e : join)
@@ -302,6 +308,36 @@ void assign_lanes(dcol_plan* p) {
     p->lanes = lanes;
 }
 
+// A plan with several solve buckets that together leave the GPU mostly idle (fewer lanes
+// than one wave per SIMD: every bucket already took its latency configuration) runs as ONE
+// fused launch; p->segs is left empty when it does not qualify (large or single-variant
+// plans, variants outside the fused kernel, DCOL_PLAN_NO_FUSE).
+void plan_fuse(const dcol_table* t, dcol_plan* p, bool allow) {
+    p->segs.clear();
+    p->fused_blocks = 0;
+    if (!allow) return;
+    int solves = 0;
+    int64_t lanes = 0;
+    for (const Launch& L : p->launches)
+        if (L.kind == 0) {
+            ++solves;
+            lanes += L.n * L.lpp;
+        }
+    if (solves < 2 || solves > kMaxFusedSegs || lanes >= 64LL * t->simds) return;
+    std::vector<FusedSeg> segs;
+    int64_t block = 0;
+    for (const Launch& L : p->launches) {
+        if (L.kind != 0) continue;
+        const int vid = fused_vid(L.N, L.nsoc, L.omax, L.lpp, L.full);
+        if (vid < 0) return;
+        segs.push_back(FusedSeg{vid, L.lpp, block, L.slot0, L.n});
+        block += (L.n * L.lpp + kBlock - 1) / kBlock;
+    }
+    p->segs = std::move(segs);
+    p->fused_blocks = block;
+    p->lanes = 1;   // no fan-out
+}
+
 int ensure_fanout(const dcol_table* tc, dcol_plan* p) {
     if (p->lanes <= 1) return DCOL_SUCCESS;
     dcol_table* t = const_cast<dcol_table*>(tc);
@@ -332,7 +368,8 @@ int dcol_plan_create(const dcol_table* t, int64_t B, const int32_t* s1, const in
 int dcol_plan_create_ex(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, int32_t options,
                         dcol_plan** out) {
     if (!t || !out || B < 0 || (B > 0 && (!s1 || !s2))) return fail(DCOL_ERR_ARG, "dcol_plan_create: bad arguments");
-    if (options & ~DCOL_PLAN_CASE4) return fail(DCOL_ERR_ARG, "dcol_plan_create_ex: unknown option bits");
+    if (options & ~(DCOL_PLAN_CASE4 | DCOL_PLAN_NO_FUSE))
+        return fail(DCOL_ERR_ARG, "dcol_plan_create_ex: unknown option bits");
     if (B > INT32_MAX) return fail(DCOL_ERR_ARG, "dcol_plan_create: B exceeds 2^31-1");
     *out = nullptr;
     auto* p = new (std::nothrow) dcol_plan();
@@ -343,6 +380,7 @@ int dcol_plan_create_ex(const dcol_table* t, int64_t B, const int32_t* s1, const
         delete p;
         return rc;
     }
+    plan_fuse(t, p, (options & DCOL_PLAN_NO_FUSE) == 0);
     p->owns = true;
     if (B == 0) {
         *out = p;
@@ -356,6 +394,11 @@ int dcol_plan_create_ex(const dcol_table* t, int64_t B, const int32_t* s1, const
     if (e == hipSuccess && p->launches.size() > 1) {
         e = hipMalloc(&p->d_perm, sizeof(int32_t) * B);
         if (e == hipSuccess) e = hipMemcpy(p->d_perm, perm.data(), sizeof(int32_t) * B, hipMemcpyHostToDevice);
+    }
+    if (e == hipSuccess && p->fused()) {
+        const size_t sb = sizeof(FusedSeg) * p->segs.size();
+        e = hipMalloc(&p->d_segs, sb);
+        if (e == hipSuccess) e = hipMemcpy(p->d_segs, p->segs.data(), sb, hipMemcpyHostToDevice);
     }
     if (e != hipSuccess) {
         dcol_plan_destroy(p);
@@ -377,6 +420,7 @@ int dcol_plan_destroy(dcol_plan* p) {
         if (p->d_s1) (void)hipFree(p->d_s1);
         if (p->d_s2) (void)hipFree(p->d_s2);
         if (p->d_perm) (void)hipFree(p->d_perm);
+        if (p->d_segs) (void)hipFree(p->d_segs);
     }
     delete p;
     return DCOL_SUCCESS;
@@ -384,6 +428,14 @@ int dcol_plan_destroy(dcol_plan* p) {
 
 int dcol_plan_num_launches(const dcol_plan* p, int32_t* n) {
     if (!p || !n) return fail(DCOL_ERR_ARG, "dcol_plan_num_launches: NULL argument");
+    int32_t k = 0;
+    for (const Launch& L : p->launches) k += (L.kind != 0 || !p->fused());
+    *n = k + (p->fused() ? 1 : 0);
+    return DCOL_SUCCESS;
+}
+
+int dcol_plan_num_buckets(const dcol_plan* p, int32_t* n) {
+    if (!p || !n) return fail(DCOL_ERR_ARG, "dcol_plan_num_buckets: NULL argument");
     *n = (int32_t)p->launches.size();
     return DCOL_SUCCESS;
 }
@@ -425,6 +477,7 @@ int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, 
         if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_plan_run fork: ") + hipGetErrorString(e));
     }
     for (const Launch& L : p->launches) {
+        if (L.kind == 0 && p->fused()) continue;   // covered by the fused launch below
         a.slot0 = L.slot0;
         a.n = L.n;
         hipStream_t ls = (fan && L.lane > 0) ? t->side[L.lane - 1] : st;
@@ -436,6 +489,11 @@ int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, 
             e = launch_variant(L.N, L.nsoc, L.omax, L.lpp, L.full, a, ls);
         }
         if (e != hipSuccess) break;
+    }
+    if (e == hipSuccess && p->fused()) {
+        a.slot0 = 0;
+        a.n = 0;
+        e = launch_fused(a, p->d_segs, (int)p->segs.size(), p->fused_blocks, st);
     }
     if (fan) {   // join even after a failed launch, so the side streams never run ahead
         for (int l = 1; l < p->lanes; ++l) {
@@ -461,12 +519,15 @@ int dcol_prox_batch_host(const dcol_table* tc, int64_t B, const int32_t* s1, con
     std::vector<int32_t> perm;
     int rc = bucket_pairs(t, B, s1, s2, &p, perm, (flags & DCOL_CASE4) != 0);
     if (rc != DCOL_SUCCESS) return rc;
+    plan_fuse(t, &p, true);
     rc = ensure_fanout(t, &p);
     if (rc != DCOL_SUCCESS) return rc;
     DeviceGuard g(t->device);
-    // staging: doubles pose1[6B] pose2[6B] | alpha[B] contact[3B] grad[12B] ; ints s1 s2 perm iters status
+    // staging: doubles pose1[6B] pose2[6B] | alpha[B] contact[3B] grad[12B] ; fused segments ;
+    // ints s1 s2 perm iters status
     const size_t nin = (size_t)12 * B, nout = (size_t)16 * B;
-    const size_t bytes = (nin + nout) * sizeof(double) + 5 * (size_t)B * sizeof(int32_t);
+    const size_t segb = sizeof(FusedSeg) * p.segs.size();
+    const size_t bytes = (nin + nout) * sizeof(double) + segb + 5 * (size_t)B * sizeof(int32_t);
     if (t->stage_bytes < bytes) {
         if (t->stage) (void)hipFree(t->stage);
         t->stage = nullptr;
@@ -480,7 +541,9 @@ int dcol_prox_batch_host(const dcol_table* tc, int64_t B, const int32_t* s1, con
     double* dal = dp1 + nin;
     double* dct = dal + B;
     double* dgr = dct + 3 * B;
-    int32_t* ib = reinterpret_cast<int32_t*>(dp1 + nin + nout);
+    FusedSeg* dsg = reinterpret_cast<FusedSeg*>(dp1 + nin + nout);
+    p.d_segs = p.fused() ? dsg : nullptr;
+    int32_t* ib = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(dsg) + segb);
     p.d_s1 = ib;
     p.d_s2 = ib + B;
     p.d_perm = p.launches.size() > 1 ? ib + 2 * B : nullptr;
@@ -499,6 +562,7 @@ int dcol_prox_batch_host(const dcol_table* tc, int64_t B, const int32_t* s1, con
     std::memcpy(ids.data() + 2 * B, perm.data(), sizeof(int32_t) * B);
     hipError_t e = hipMemcpy(dp1, soa.data(), sizeof(double) * nin, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(ib, ids.data(), sizeof(int32_t) * 3 * B, hipMemcpyHostToDevice);
+    if (e == hipSuccess && segb) e = hipMemcpy(dsg, p.segs.data(), segb, hipMemcpyHostToDevice);
     if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_prox_batch_host H2D: ") + hipGetErrorString(e));
     rc = dcol_plan_run(&p, dp1, dp2, tol, max_iter, flags, dal, dct, dgr, dit, dst, nullptr);
     if (rc != DCOL_SUCCESS) return rc;

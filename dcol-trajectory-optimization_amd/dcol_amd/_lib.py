@@ -19,7 +19,7 @@ OK, MAXITER, UNSUPPORTED, NOT_PD, NONFINITE, TOO_LARGE = range(6)
 # enum dcol_flags
 GRAD_FD, GRAD_ENVELOPE, CONTACT, CASE4 = 1, 2, 4, 8
 # enum dcol_plan_options
-PLAN_CASE4 = 1
+PLAN_CASE4, PLAN_NO_FUSE = 1, 2
 SUCCESS, ERR_ARG, ERR_HIP, ERR_NOMEM = 0, -1, -2, -3
 ABI_VERSION = 1
 
@@ -50,6 +50,7 @@ SIGNATURES = {
     "dcol_plan_create_ex": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int32, POINTER(c_void_p)]),
     "dcol_plan_destroy": (c_int, [c_void_p]),
     "dcol_plan_num_launches": (c_int, [c_void_p, POINTER(c_int32)]),
+    "dcol_plan_num_buckets": (c_int, [c_void_p, POINTER(c_int32)]),
     "dcol_plan_run": (c_int, [c_void_p, c_void_p, c_void_p, c_double, c_int32, c_int32, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_void_p]),
     "dcol_prox_batch_host": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_double,

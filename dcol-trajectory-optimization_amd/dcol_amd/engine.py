@@ -103,9 +103,10 @@ class Table:
 class Plan:
     """Owning wrapper of a dcol_plan: a fixed pairing bucketed by kernel variant."""
 
-    def __init__(self, table: Table, s1, s2, case4: bool = False):
+    def __init__(self, table: Table, s1, s2, case4: bool = False, fuse: bool = True):
         """case4=True: solve case-4 pairs (DCOL_PLAN_CASE4 extension) instead of reporting
-        UNSUPPORTED like the reference."""
+        UNSUPPORTED like the reference.  fuse=False: one launch per variant bucket even for
+        a small mixed plan (DCOL_PLAN_NO_FUSE; A/B and tests)."""
         lib = _lib.load()
         self.s1 = np.ascontiguousarray(s1, dtype=np.int32)
         self.s2 = np.ascontiguousarray(s2, dtype=np.int32)
@@ -115,12 +116,15 @@ class Plan:
         self.B = int(self.s1.size)
         h = ctypes.c_void_p()
         self.case4 = bool(case4)
+        opts = (_lib.PLAN_CASE4 if case4 else 0) | (0 if fuse else _lib.PLAN_NO_FUSE)
         _lib.check(lib.dcol_plan_create_ex(table.handle, self.B, _np_ptr(self.s1), _np_ptr(self.s2),
-                                           _lib.PLAN_CASE4 if case4 else 0, ctypes.byref(h)), "dcol_plan_create_ex")
+                                           opts, ctypes.byref(h)), "dcol_plan_create_ex")
         self.handle = h
         n = ctypes.c_int32()
         _lib.check(lib.dcol_plan_num_launches(h, ctypes.byref(n)), "dcol_plan_num_launches")
-        self.num_launches = int(n.value)
+        self.num_launches = int(n.value)       # kernel launches per run
+        _lib.check(lib.dcol_plan_num_buckets(h, ctypes.byref(n)), "dcol_plan_num_buckets")
+        self.num_buckets = int(n.value)        # variant buckets (incl. rejected pairs)
 
     def run(self, pose1, pose2, tol=DEFAULT_TOL, max_iter=DEFAULT_MAX_ITER, grad="fd", contact=True,
             out=None, stream=None):
@@ -247,16 +251,16 @@ class Engine:
                 self._table = Table(self._specs, self.device)
             return self._table
 
-    def plan(self, s1, s2, cache=True, case4=False) -> Plan:
+    def plan(self, s1, s2, cache=True, case4=False, fuse=True) -> Plan:
         s1 = np.ascontiguousarray(s1, dtype=np.int32)
         s2 = np.ascontiguousarray(s2, dtype=np.int32)
         if not cache:
-            return Plan(self.table, s1, s2, case4)
-        key = (s1.tobytes(), s2.tobytes(), bool(case4))
+            return Plan(self.table, s1, s2, case4, fuse)
+        key = (s1.tobytes(), s2.tobytes(), bool(case4), bool(fuse))
         with self._lock:
             p = self._plans.get(key)
             if p is None or p.table is not self.table:
-                p = Plan(self.table, s1, s2, case4)
+                p = Plan(self.table, s1, s2, case4, fuse)
                 self._plans[key] = p
                 if len(self._plans) > 32:
                     self._plans.popitem(last=False)

@@ -70,12 +70,16 @@ enum dcol_flags {
 
 /* dcol_plan_create_ex options. */
 enum dcol_plan_options {
-    DCOL_PLAN_CASE4 = 1 /* EXTENSION, not reference behaviour: pairs in which BOTH primitives
+    DCOL_PLAN_CASE4 = 1, /* EXTENSION, not reference behaviour: pairs in which BOTH primitives
                            have extra columns (capsule/cylinder/polygon x capsule/cylinder/
                            polygon) — combine_problem_matrices.py:58-67 raises ValueError for
                            them — are assembled with primitive 2's extra columns placed after
                            primitive 1's (n = 4 + e1 + e2 <= 8) and solved by the same PDIP.
                            Without the option they get DCOL_UNSUPPORTED like the reference. */
+    DCOL_PLAN_NO_FUSE = 2 /* always one launch per bucket.  By default a plan with several
+                           buckets (kernel variants) whose pairs together fill less than one
+                           wave per SIMD -- an ALTRO phase batch -- runs every bucket in ONE
+                           fused launch (no stream fan-out); results are bitwise the same.  */
 };
 
 /* Return codes of every entry point. */
@@ -124,7 +128,8 @@ int dcol_plan_create(const dcol_table* table, int64_t B, const int32_t* shape1,
 int dcol_plan_create_ex(const dcol_table* table, int64_t B, const int32_t* shape1,
                         const int32_t* shape2, int32_t options, dcol_plan** out);
 int dcol_plan_destroy(dcol_plan* plan);
-int dcol_plan_num_launches(const dcol_plan* plan, int32_t* n);
+int dcol_plan_num_launches(const dcol_plan* plan, int32_t* n); /* kernel launches per run */
+int dcol_plan_num_buckets(const dcol_plan* plan, int32_t* n);  /* variant buckets (incl. rejects) */
 
 /* Solve every pair of the plan.  All arrays are DEVICE pointers on the table's device,
  * structure-of-arrays:
