@@ -88,6 +88,26 @@ def cpu_baseline(tab, s1, s2, p1, p2, sample, workers):
             "per_core": n / cpu_s}
 
 
+def cpu_baseline_c(tab, s1, s2, p1, p2, threads, seconds=3.0):
+    """C restatement of the reference (oracle/dcol_oracle.c, a 'port', OpenMP over `threads`
+    host cores; SURVEY.md §8d asks for both restatements): the same pairs, repeated until
+    about `seconds` of wall time."""
+    from oracle import c_oracle
+    n = min(len(s1), 20000)
+    c_oracle.run_batch(tab, s1[:256], s2[:256], p1[:256], p2[:256], want_grad=True, threads=threads)  # load/warm
+    done, t0 = 0, time.perf_counter()
+    while True:
+        c_oracle.run_batch(tab, s1[:n], s2[:n], p1[:n], p2[:n], want_grad=True, threads=threads)
+        done += n
+        wall = time.perf_counter() - t0
+        if wall >= seconds:
+            break
+    return {"value": done / wall, "unit": "pair-solves/s", "cores": threads, "kind": "port",
+            "sample": f"{done} solves ({n} distinct synthetic poly-poly pairs), proximity+FD gradient, C oracle "
+                      f"(oracle/dcol_oracle.c), OpenMP {threads} threads, {wall:.1f} s wall",
+            "per_core": done / wall / threads}
+
+
 def read_traffic(profile_dir, kernel_substr="prox_kernel"):
     """Per-launch HBM bytes of the solve kernel from a committed rocprofv3 PMC pass
     (FETCH_SIZE + WRITE_SIZE in KB; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM)."""
@@ -265,6 +285,7 @@ def main():
     if world == 1 and not args.no_cpu:
         workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
         line["cpu_baseline"] = cpu_baseline(tab, s1, s2, p1, p2, args.cpu_sample, workers)
+        line["cpu_baseline_c"] = cpu_baseline_c(tab, s1, s2, p1, p2, workers)
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -1058,54 +1058,54 @@ struct Solver {
     // primitive k.  Every row of every primitive is linear in (Qe, re): orthant rows
     // z_i((Qe a_i).(x - re) + g3_i x3 + ex_i.xe) sum to (Qe w).(x - re) + const with
     // w = sum z_i a_i; a ball SOC block adds z_1..3 . (re + Qe[:, extras] xe) + const; a cone
-    // SOC block adds -(Qe E z_0..2).(x - re) + const.  The constants are pose-independent
-    // and cancel exactly in a forward difference, so they are never formed.
+    // SOC block's rows are Qe(-E e_k) rows of the same form (w gains -E z_0..2).  The
+    // constants are pose-independent and cancel exactly in a forward difference, so they are
+    // never formed.  w is taken from the assembled rows in registers rather than the row
+    // table: u = sum z_i G_i[0:3] = Qe w (world frame), w = Qe' u (Qe orthogonal; the same w
+    // enters every evaluation of the difference, so its rounding is not amplified by 1/h).
     struct LagAgg {
-        double w[3];     // sum over owned orthant rows of z_i a_i (body frame), group-summed
+        double u[3];     // sum of z_i G_i[0:3] over the primitive's orthant and cone rows, group-summed
         double zs[4];    // the primitive's SOC block duals (zero if none), group-summed
         int kind;        // SOC kind of the primitive's block
     };
-    DCOL_HD LagAgg lag_aggregate(const KArgs& A, const DevShape& S, int prim) const {
-        const double* __restrict__ rows = reinterpret_cast<const double*>(A.rows);
+    DCOL_HD LagAgg lag_aggregate(const DevShape& S, int prim) const {
         LagAgg g;
-        g.w[0] = g.w[1] = g.w[2] = 0.0;
+        g.u[0] = g.u[1] = g.u[2] = 0.0;
         g.zs[0] = g.zs[1] = g.zs[2] = g.zs[3] = 0.0;
         g.kind = S.soc_kind;
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
-            if (owns_row(k, prim)) {
-                const int i = k * LPP + q;
-                const int ri = S.row_off + ((prim == 0) ? i : (i - o1));
-                const double2* rw = reinterpret_cast<const double2*>(rows + 8 * (int64_t)ri);
-                const double2 q0 = rw[0], q1 = rw[1];
-                g.w[0] += z[k] * q0.x;
-                g.w[1] += z[k] * q0.y;
-                g.w[2] += z[k] * q1.x;
+            const double zk = owns_row(k, prim) ? z[k] : 0.0;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) g.u[c] = fma(zk, G[k][c], g.u[c]);
+        }
+#pragma unroll
+        for (int b = 0; b < SS; ++b) {
+            const bool own = vs[b] && soc_owner[b] == prim;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const double ze = own ? z[OR + 4 * b + e] : 0.0;
+                g.zs[e] = own ? ze : g.zs[e];
+                const double zc = (g.kind == SOC_CONE) ? ze : 0.0;   // cone rows: Qe(-E e_k)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) g.u[c] = fma(zc, G[OR + 4 * b + e][c], g.u[c]);
             }
         }
 #pragma unroll
-        for (int b = 0; b < SS; ++b)
-            if (vs[b] && soc_owner[b] == prim)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) g.zs[e] = z[OR + 4 * b + e];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) g.w[c] = R::sum(g.w[c]);
+        for (int c = 0; c < 3; ++c) g.u[c] = R::sum(g.u[c]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) g.zs[e] = R::sum(g.zs[e]);
         return g;
     }
-    DCOL_HD double lag_pose_part(const LagAgg& g, const DevShape& S, int prim, const Frame& Fr) const {
-        double d[3], v[3];
+    // body-frame w = Qe' u
+    DCOL_HD static void body_w(const LagAgg& g, const Frame& Fr, double* w) {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            d[c] = x[c] - Fr.re[c];
-            v[c] = g.w[c];
-        }
-        if (g.kind == SOC_CONE) {          // a_k = -E_kk e_k for the three cone rows
-            v[0] -= S.tanb * g.zs[0];
-            v[1] -= g.zs[1];
-            v[2] -= g.zs[2];
-        }
+        for (int c = 0; c < 3; ++c) w[c] = Fr.Qe[c] * g.u[0] + Fr.Qe[3 + c] * g.u[1] + Fr.Qe[6 + c] * g.u[2];
+    }
+    DCOL_HD double lag_pose_part(const LagAgg& g, const double* v, const DevShape& S, int prim, const Frame& Fr) const {
+        double d[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) d[c] = x[c] - Fr.re[c];
         double f = 0.0;
 #pragma unroll
         for (int r = 0; r < 3; ++r) f += (Fr.Qe[3 * r] * v[0] + Fr.Qe[3 * r + 1] * v[1] + Fr.Qe[3 * r + 2] * v[2]) * d[r];
@@ -1141,13 +1141,15 @@ struct Solver {
         }
         Frame F0;
         make_frame(S, th0, F0);
-        const double f0 = lag_pose_part(ag, S, prim, F0);
+        double w[3];
+        body_w(ag, F0, w);
+        const double f0 = lag_pose_part(ag, w, S, prim, F0);
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
             Frame Fj = F0;
 #pragma unroll
             for (int c = 0; c < 3; ++c) Fj.re[c] = (c == j ? tj[j] : th0[c]) + F0.qro[c];
-            g[j] = (lag_pose_part(ag, S, prim, Fj) - f0) * idx[j];
+            g[j] = (lag_pose_part(ag, w, S, prim, Fj) - f0) * idx[j];
         }
 #pragma unroll
         for (int j = 3; j < 6; ++j) {
@@ -1156,7 +1158,7 @@ struct Solver {
             for (int c = 0; c < 6; ++c) th[c] = (c == j) ? tj[j] : th0[c];
             Frame Fj;
             make_frame(S, th, Fj);
-            g[j] = (lag_pose_part(ag, S, prim, Fj) - f0) * idx[j];
+            g[j] = (lag_pose_part(ag, w, S, prim, Fj) - f0) * idx[j];
         }
     }
 
@@ -1167,12 +1169,9 @@ struct Solver {
     DCOL_HD void env_grad_prim(const LagAgg& ag, const DevShape& S, int prim, const double th[6], double* g) const {
         Frame Fr;
         make_frame(S, th, Fr);
-        double w[3] = {ag.w[0], ag.w[1], ag.w[2]}, zeta[3] = {0.0, 0.0, 0.0};
-        if (ag.kind == SOC_CONE) {          // a_k = -E_kk e_k
-            w[0] -= ag.zs[0] * S.tanb;
-            w[1] -= ag.zs[1];
-            w[2] -= ag.zs[2];
-        } else if (ag.kind == SOC_BALL) {
+        double w[3], zeta[3] = {0.0, 0.0, 0.0};
+        body_w(ag, Fr, w);                  // includes the cone rows' -E z_0..2
+        if (ag.kind == SOC_BALL) {
             zeta[0] = ag.zs[1]; zeta[1] = ag.zs[2]; zeta[2] = ag.zs[3];
         }
         double xi[3] = {0.0, 0.0, 0.0};
@@ -1287,8 +1286,8 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
             // group does the two 6-coordinate gradients side by side instead of both in
             // every lane (a 1-lane group does both in turn)
             using Agg = typename Solver<N, NSOC, OMAX, LPP>::LagAgg;
-            const Agg ag0 = P.lag_aggregate(L, T1, 0);
-            const Agg ag1 = P.lag_aggregate(L, T2, 1);
+            const Agg ag0 = P.lag_aggregate(T1, 0);
+            const Agg ag1 = P.lag_aggregate(T2, 1);
             constexpr int NP = LPP >= 2 ? 1 : 2;
 #pragma unroll
             for (int pp = 0; pp < NP; ++pp) {
@@ -1296,7 +1295,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
                 const DevShape& T = prim ? T2 : T1;
                 Agg ag;   // element-wise select (a reference select would put both on the stack)
 #pragma unroll
-                for (int c = 0; c < 3; ++c) ag.w[c] = prim ? ag1.w[c] : ag0.w[c];
+                for (int c = 0; c < 3; ++c) ag.u[c] = prim ? ag1.u[c] : ag0.u[c];
 #pragma unroll
                 for (int c = 0; c < 4; ++c) ag.zs[c] = prim ? ag1.zs[c] : ag0.zs[c];
                 ag.kind = prim ? ag1.kind : ag0.kind;
