@@ -478,6 +478,23 @@ struct Solver {
     DCOL_HD bool vrow(int k) const { return k < OR ? vort(k) : vs[(k - OR) / 4]; }
 
     // -------- assembly (problem_matrices.py + combine_problem_matrices.py) --------------
+    // One orthant slot: row i = k * LPP + q of primitive p2 (frame F) -> G[k], h in r[k].
+    DCOL_HD void orth_row(const double* __restrict__ rows, int k, bool v, bool p2, int ri, const Frame& F) {
+        double a0 = 0, a1 = 0, a2 = 0, g3 = 0, e0 = 0, e1 = 0;
+        if (v) {
+            const double2* rw = reinterpret_cast<const double2*>(rows + 8 * (int64_t)ri);
+            const double2 q0 = rw[0], q1 = rw[1], q2 = rw[2];
+            a0 = q0.x; a1 = q0.y; a2 = q1.x; g3 = q1.y; e0 = q2.x; e1 = q2.y;
+        }
+        const double u0 = F.Qe[0] * a0 + F.Qe[1] * a1 + F.Qe[2] * a2;
+        const double u1 = F.Qe[3] * a0 + F.Qe[4] * a1 + F.Qe[5] * a2;
+        const double u2 = F.Qe[6] * a0 + F.Qe[7] * a1 + F.Qe[8] * a2;
+        G[k][0] = u0; G[k][1] = u1; G[k][2] = u2; G[k][3] = g3;
+        const int off = xoff(p2);
+#pragma unroll
+        for (int j = 4; j < N; ++j) G[k][j] = excol(j, off, e0, e1);
+        r[k] = u0 * F.re[0] + u1 * F.re[1] + u2 * F.re[2];
+    }
     // leaves h in r[] (init turns it into G x_hat - h)
     DCOL_HD void assemble(const KArgs& A, const DevShape& S1, const DevShape& S2, const Frame& F1, const Frame& F2) {
         o1 = S1.n_ort;
@@ -490,26 +507,12 @@ struct Solver {
             const int i = k * LPP + q;
             const bool v = i < o;
             const bool p2 = i >= o1;
-            double a0 = 0, a1 = 0, a2 = 0, g3 = 0, e0 = 0, e1 = 0;
-            if (v) {
-                const int ri = p2 ? (S2.row_off + (i - o1)) : (S1.row_off + i);
-                const double2* rw = reinterpret_cast<const double2*>(rows + 8 * (int64_t)ri);
-                const double2 q0 = rw[0], q1 = rw[1], q2 = rw[2];
-                a0 = q0.x; a1 = q0.y; a2 = q1.x; g3 = q1.y; e0 = q2.x; e1 = q2.y;
-            }
-            double Qe[9], re[3];
+            Frame F;   // element-wise select of the row's frame
 #pragma unroll
-            for (int c = 0; c < 9; ++c) Qe[c] = p2 ? F2.Qe[c] : F1.Qe[c];
+            for (int c = 0; c < 9; ++c) F.Qe[c] = p2 ? F2.Qe[c] : F1.Qe[c];
 #pragma unroll
-            for (int c = 0; c < 3; ++c) re[c] = p2 ? F2.re[c] : F1.re[c];
-            const double u0 = Qe[0] * a0 + Qe[1] * a1 + Qe[2] * a2;
-            const double u1 = Qe[3] * a0 + Qe[4] * a1 + Qe[5] * a2;
-            const double u2 = Qe[6] * a0 + Qe[7] * a1 + Qe[8] * a2;
-            G[k][0] = u0; G[k][1] = u1; G[k][2] = u2; G[k][3] = g3;
-            const int off = xoff(p2);
-#pragma unroll
-            for (int j = 4; j < N; ++j) G[k][j] = excol(j, off, e0, e1);
-            r[k] = u0 * re[0] + u1 * re[1] + u2 * re[2];
+            for (int c = 0; c < 3; ++c) F.re[c] = p2 ? F2.re[c] : F1.re[c];
+            orth_row(rows, k, v, p2, p2 ? (S2.row_off + (i - o1)) : (S1.row_off + i), F);
         }
         // global SOC block 0 = first primitive with a SOC, block 1 = prim 2 when both have one
         const int own0 = S1.soc_kind != SOC_NONE ? 0 : 1;
@@ -747,6 +750,11 @@ struct Solver {
     DCOL_HD int32_t pdip(double tol, int max_iter, int* it_out) {
         int it = 0;
         int32_t st = ST_MAXITER;
+        // mu = s'z / deg as a multiply by the correctly rounded 1/deg plus one FMA remainder
+        // correction (Markstein): the correctly rounded quotient, without a division sequence
+        // per iteration
+        const double degd = FULL ? (double)(OMAX + NSOC) : (double)deg;
+        const double rdeg = 1.0 / degd;
         for (it = 0; it < max_iter; ++it) {
             DCOL_ISTAMP(it, 0);
             // ---- mu = s'z / deg and the exit test first (pdip.py:410-422, quirk Q3): the
@@ -767,7 +775,8 @@ struct Solver {
                 sz = vs[b] ? sz + szb : sz;
             }
             sz = R::sum(sz);
-            const double mu = sz / (double)deg;
+            const double mq = sz * rdeg;
+            const double mu = fma(fma(-mq, degd, sz), rdeg, mq);
             if (mu < tol) {
                 st = ST_OK;
                 break;
