@@ -124,8 +124,9 @@ def read_traffic(profile_dir, kernel_substr="prox_kernel"):
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=500,
+                    help="timed steps (0.05-2 ms each; enough for the GPU clocks to settle)")
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--pairs", type=int, default=100_000, help="pairs per GPU")
     ap.add_argument("--grad", choices=["fd", "envelope"], default="fd")
     ap.add_argument("--cpu-sample", type=int, default=16000)

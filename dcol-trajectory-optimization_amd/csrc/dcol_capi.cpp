@@ -91,6 +91,8 @@ struct Launch {
     int kind;       // 0 = solve, 1 = reject
     int N, nsoc, omax, lpp;
     bool full = false;   // every pair has o == omax: the padding-free kernel (DCOL_FULL_VARIANTS) if built
+    bool ball = false;   // every SOC block is a ball block: the structured kernel (DCOL_BALL_VARIANTS) if built
+    int flags() const { return (full ? LF_FULL : 0) | (ball ? LF_BALL : 0); }
     int32_t code;   // reject status
     int64_t slot0, n;
     int lane = 0;   // 0 = caller's stream, 1..kSideStreams = table side stream
@@ -121,12 +123,12 @@ struct dcol_plan {
 
 namespace {
 
-hipError_t launch_variant(int N, int nsoc, int omax, int lpp, bool full, const KArgs& a, hipStream_t st) {
-    if (N == 4) return launch_n4(nsoc, omax, lpp, full, a, st);
-    if (N == 5) return launch_n5(nsoc, omax, lpp, full, a, st);
-    if (N == 6) return launch_n6(nsoc, omax, lpp, full, a, st);
-    if (N == 7) return launch_n7(nsoc, omax, lpp, full, a, st);
-    if (N == 8) return launch_n8(nsoc, omax, lpp, full, a, st);
+hipError_t launch_variant(int N, int nsoc, int omax, int lpp, int flags, const KArgs& a, hipStream_t st) {
+    if (N == 4) return launch_n4(nsoc, omax, lpp, flags, a, st);
+    if (N == 5) return launch_n5(nsoc, omax, lpp, flags, a, st);
+    if (N == 6) return launch_n6(nsoc, omax, lpp, flags, a, st);
+    if (N == 7) return launch_n7(nsoc, omax, lpp, flags, a, st);
+    if (N == 8) return launch_n8(nsoc, omax, lpp, flags, a, st);
     return hipErrorInvalidValue;
 }
 
@@ -236,19 +238,29 @@ int dcol_pair_dims(const dcol_table* t, int32_t s1, int32_t s2, int32_t* m, int3
 namespace {
 void assign_lanes(dcol_plan* p);
 
+// DCOL_NO_BALL=1: ball-SOC pairs run the dense kernels too (A/B runs, tests)
+bool ball_disabled() {
+    static const bool off = std::getenv("DCOL_NO_BALL") != nullptr;
+    return off;
+}
+
 // Classify + bucket (counting sort by variant key).  Fills p->launches and the slot->pair
 // permutation; returns DCOL_SUCCESS or an error.
 int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, dcol_plan* p,
                  std::vector<int32_t>& perm, bool case4) {
     const int32_t ns = (int32_t)t->shapes.size();
-    using Key = std::tuple<int, int, int, int, int, int>;   // kind, N, nsoc, omax, lpp, code
+    // kind, N, nsoc, omax, lpp, ball (SOC blocks all balls: no cone), code
+    using Key = std::tuple<int, int, int, int, int, int, int>;
     std::map<Key, std::vector<int32_t>> groups;
     std::map<Key, bool> full;
     for (int64_t i = 0; i < B; ++i) {
         if (s1[i] < 0 || s1[i] >= ns || s2[i] < 0 || s2[i] >= ns)
             return fail(DCOL_ERR_ARG, "shape id out of range at pair " + std::to_string(i));
-        PairClass c = classify(t->shapes[s1[i]], t->shapes[s2[i]], case4);
-        Key k = c.status == DCOL_OK ? Key{0, c.N, c.nsoc, c.omax, c.lpp, 0} : Key{1, 0, 0, 0, 0, c.status};
+        const DevShape& a = t->shapes[s1[i]];
+        const DevShape& b = t->shapes[s2[i]];
+        PairClass c = classify(a, b, case4);
+        const int ball = (c.nsoc > 0 && a.soc_kind != SOC_CONE && b.soc_kind != SOC_CONE && !ball_disabled()) ? 1 : 0;
+        Key k = c.status == DCOL_OK ? Key{0, c.N, c.nsoc, c.omax, c.lpp, ball, 0} : Key{1, 0, 0, 0, 0, 0, c.status};
         groups[k].push_back((int32_t)i);
         auto f = full.emplace(k, true).first;
         f->second = f->second && c.o == c.omax;
@@ -265,8 +277,9 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
         L.nsoc = std::get<2>(kv.first);
         L.omax = std::get<3>(kv.first);
         L.lpp = std::get<4>(kv.first);
-        L.code = std::get<5>(kv.first);
+        L.code = std::get<6>(kv.first);
         L.full = L.kind == 0 && full[kv.first];
+        L.ball = L.kind == 0 && std::get<5>(kv.first) == 1;
         L.slot0 = (int64_t)perm.size();
         L.n = (int64_t)kv.second.size();
         if (L.kind == 0 && !lpp_forced() && L.n * L.lpp < 64LL * t->simds)   // cannot fill the GPU
@@ -328,7 +341,7 @@ void plan_fuse(const dcol_table* t, dcol_plan* p, bool allow) {
     int64_t block = 0;
     for (const Launch& L : p->launches) {
         if (L.kind != 0) continue;
-        const int vid = fused_vid(L.N, L.nsoc, L.omax, L.lpp, L.full);
+        const int vid = fused_vid(L.N, L.nsoc, L.omax, L.lpp, L.flags());
         if (vid < 0) return;
         segs.push_back(FusedSeg{vid, L.lpp, block, L.slot0, L.n});
         block += (L.n * L.lpp + kBlock - 1) / kBlock;
@@ -486,7 +499,7 @@ int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, 
             hipLaunchKernelGGL(reject_kernel, dim3(grid), dim3(kBlock), 0, ls, a, L.code);
             e = hipGetLastError();
         } else {
-            e = launch_variant(L.N, L.nsoc, L.omax, L.lpp, L.full, a, ls);
+            e = launch_variant(L.N, L.nsoc, L.omax, L.lpp, L.flags(), a, ls);
         }
         if (e != hipSuccess) break;
     }

@@ -445,16 +445,28 @@ struct Grp<4> {
 //  * the primal residual r = G x - h is carried incrementally (r += a G dx);
 //  * orthant ratio tests as a running max of -d/x through the row reciprocals (bound_inv);
 //  * G~ = W^-1 G is never formed: G~'G~ and G~'v accumulate G'(W^-1 ...).
-template <int N, int NSOC, int OMAX, int LPP>
+//
+// BALL: every SOC block of the launch is a ball block (sphere / capsule / cylinder /
+// polygon; no cone -- the host buckets such pairs separately).  A ball block's rows are
+// [0 0 0 -R | 0] and [-e_k | 0 | X_k] (k = 0..2, X = the primitive's extra columns
+// Qe[:, 0..nx)), problem_matrices.py:21-28, 66-76, 112-119, 165-176, so only (R, X) are
+// held -- scaled by sv = 1 (real block) / 0 (inert slot) -- and every product with the
+// block is written out with its zeros dropped (same nonzero terms in the same order as the
+// dense rows).  Frees 4N doubles of registers per SOC slot.
+template <int N, int NSOC, int OMAX, int LPP, bool BALL = false>
 struct Solver {
     static_assert(OMAX % LPP == 0, "OMAX must be a multiple of LPP");
     static constexpr int OR = OMAX / LPP;              // orthant slots per lane
     static constexpr int SS = (NSOC + LPP - 1) / LPP;  // SOC slots per lane
     static constexpr int M = OR + 4 * SS;              // lane-local rows
     static constexpr int SSA = SS > 0 ? SS : 1;
+    static constexpr int MG = BALL ? OR : M;           // rows held densely in G
+    static constexpr int NX = N - 4;                   // extra primal columns
+    static constexpr int NXA = NX > 0 ? NX : 1;
     using R = Grp<LPP>;
 
-    double G[M][N];
+    double G[MG][N];
+    double sv[SSA], sR[SSA], sX[SSA][3][NXA];   // BALL: structured SOC rows (see above)
     double s[M], z[M], r[M];   // slack, dual, primal residual G x - h
     double x[N];
     int q, o1, o, deg;
@@ -528,8 +540,24 @@ struct Solver {
 #pragma unroll
             for (int c = 0; c < 3; ++c) re[c] = p2 ? F2.re[c] : F1.re[c];
             const int kind = vs[b] ? (p2 ? S2.soc_kind : S1.soc_kind) : SOC_NONE;
-            soc_rows(kind, p2 ? S2.R : S1.R, p2 ? S2.cone_c : S1.cone_c, p2 ? S2.tanb : S1.tanb,
-                     p2 ? S2.n_extra : S1.n_extra, xoff(p2), Qe, re, &G[OR + 4 * b], &r[OR + 4 * b]);
+            if constexpr (BALL) {
+                const double one = vs[b] ? 1.0 : 0.0;
+                const int nx = p2 ? S2.n_extra : S1.n_extra;
+                const int off = xoff(p2);
+                sv[b] = one;
+                sR[b] = vs[b] ? (p2 ? S2.R : S1.R) : 0.0;
+                r[OR + 4 * b] = 0.0;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const double c0 = (nx >= 1) ? Qe[3 * k] : 0.0, c1 = (nx >= 2) ? Qe[3 * k + 1] : 0.0;
+#pragma unroll
+                    for (int j = 4; j < N; ++j) sX[b][k][j - 4] = one * excol(j, off, c0, c1);
+                    r[OR + 4 * b + 1 + k] = vs[b] ? -re[k] : 0.0;
+                }
+            } else {
+                soc_rows(kind, p2 ? S2.R : S1.R, p2 ? S2.cone_c : S1.cone_c, p2 ? S2.tanb : S1.tanb,
+                         p2 ? S2.n_extra : S1.n_extra, xoff(p2), Qe, re, &G[OR + 4 * b], &r[OR + 4 * b]);
+            }
         }
     }
 
@@ -582,10 +610,77 @@ struct Solver {
 
     // -------- small dense helpers ------------------------------------------------------
     DCOL_HD double rowdot(int k, const double* v) const {
+        if constexpr (BALL)
+            if (k >= OR) return ball_row(k, v);
         double acc = G[k][0] * v[0];
 #pragma unroll
         for (int j = 1; j < N; ++j) acc += G[k][j] * v[j];
         return acc;
+    }
+    // BALL: row e of SOC slot b times v
+    DCOL_HD double ball_row(int k, const double* v) const {
+        const int b = (k - OR) / 4, e = (k - OR) % 4;
+        // an fma (as the dense row's last term), not a bare product the optimiser could
+        // contract into a consumer differently in different kernels (fused == split bitwise)
+        if (e == 0) return fma(-sR[b], v[3], 0.0);
+        double acc = -sv[b] * v[e - 1];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) acc = fma(sX[b][e - 1][i], v[4 + i], acc);
+        return acc;
+    }
+    // out += G_b' v over the 4 rows of SOC slot b (dense or structured)
+    DCOL_HD void soc_gtv(int b, const double* v, double* out) const {
+        const int k0 = OR + 4 * b;
+        if constexpr (BALL) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) out[j] = fma(-sv[b], v[j + 1], out[j]);
+            out[3] = fma(-sR[b], v[0], out[3]);
+#pragma unroll
+            for (int i = 0; i < NX; ++i)
+#pragma unroll
+                for (int k = 0; k < 3; ++k) out[4 + i] = fma(sX[b][k][i], v[k + 1], out[4 + i]);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int j = 0; j < N; ++j) out[j] += G[k0 + e][j] * v[e];
+        }
+    }
+    // gt = W^-1 G_b (4 x N), the SOC block of G~ (NT_scaling.py:164-202)
+    DCOL_HD void soc_gtilde(int b, const SocNT& W, double (&gt)[4][N]) const {
+        const int k0 = OR + 4 * b;
+        if constexpr (BALL) {
+            // columns 0..2: W^-1 (-e_{j+1}); column 3: W^-1 (-R e_0); extras: W^-1 (0, X_i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const double d = -(sv[b] * W.w1[j]);
+                const double c = W.bf * d;
+                gt[0][j] = W.ieta * (-d);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) gt[k + 1][j] = W.ieta * fma(c, W.w1[k], (k == j) ? -sv[b] : 0.0);
+            }
+            gt[0][3] = W.ieta * (W.w0 * -sR[b]);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) gt[k + 1][3] = W.ieta * (sR[b] * W.w1[k]);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                const double d = W.w1[0] * sX[b][0][i] + W.w1[1] * sX[b][1][i] + W.w1[2] * sX[b][2][i];
+                const double c = W.bf * d;
+                gt[0][4 + i] = W.ieta * (-d);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) gt[k + 1][4 + i] = W.ieta * fma(c, W.w1[k], sX[b][k][i]);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                double col[4], res[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) col[e] = G[k0 + e][j];
+                soc_solve(W, col, res);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) gt[e][j] = res[e];
+            }
+        }
     }
     // upper Cholesky H = F'F (scipy.linalg.cholesky); false if a pivot is <= 0, infinite or
     // NaN.  Any non-finite entry of H's upper triangle makes some pivot non-finite (a
@@ -681,12 +776,32 @@ struct Solver {
             for (int c = j; c < N; ++c) H[j][c] = 0.0;
         }
 #pragma unroll
-        for (int k = 0; k < M; ++k) {
+        for (int k = 0; k < MG; ++k) {
 #pragma unroll
             for (int j = 0; j < N; ++j) {
                 gth[j] += G[k][j] * r[k];          // r holds h here
 #pragma unroll
                 for (int c = j; c < N; ++c) H[j][c] += G[k][j] * G[k][c];
+            }
+        }
+        if constexpr (BALL) {                      // the ball rows' products, zeros dropped
+#pragma unroll
+            for (int b = 0; b < SS; ++b) {
+                const int k0 = OR + 4 * b;
+                soc_gtv(b, r + k0, gth);
+                H[3][3] = fma(sR[b], sR[b], H[3][3]);
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    H[j][j] = fma(sv[b], sv[b], H[j][j]);
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) H[j][4 + i] = fma(-sv[b], sX[b][j][i], H[j][4 + i]);
+                }
+#pragma unroll
+                for (int i = 0; i < NX; ++i)
+#pragma unroll
+                    for (int i2 = i; i2 < NX; ++i2)
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) H[4 + i][4 + i2] = fma(sX[b][k][i], sX[b][k][i2], H[4 + i][4 + i2]);
             }
         }
         allsum_sym(H);
@@ -811,25 +926,13 @@ struct Solver {
                 soc_nt(s + k0, z + k0, so[b].W);
                 soc_mul(so[b].W, z + k0, so[b].lam);
                 soc_prod(so[b].lam, so[b].lam, so[b].ll);
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-#pragma unroll
-                    for (int j = 0; j < N; ++j) rx[j] += G[k0 + e][j] * z[k0 + e];
+                soc_gtv(b, z + k0, rx);
             }
             // SOC part of the normal matrix
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
-                const int k0 = OR + 4 * b;
                 double gt[4][N];
-#pragma unroll
-                for (int j = 0; j < N; ++j) {
-                    double col[4], res[4];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) col[e] = G[k0 + e][j];
-                    soc_solve(so[b].W, col, res);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) gt[e][j] = res[e];
-                }
+                soc_gtilde(b, so[b].W, gt);
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -964,10 +1067,7 @@ struct Solver {
             soc_w2inv(so[b].W, sr, q);
 #pragma unroll
             for (int e = 0; e < 4; ++e) sbzt[b][e] = -q[e] - m[e];
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int j = 0; j < N; ++j) rhs[j] += G[k0 + e][j] * sbzt[b][e];
+            soc_gtv(b, sbzt[b], rhs);
         }
 #pragma unroll
         for (int j = 0; j < N; ++j) rhs[j] -= rx[j];     // lane partials of G'z
@@ -1095,9 +1195,11 @@ struct Solver {
             for (int e = 0; e < 4; ++e) {
                 const double ze = own ? z[OR + 4 * b + e] : 0.0;
                 g.zs[e] = own ? ze : g.zs[e];
-                const double zc = (g.kind == SOC_CONE) ? ze : 0.0;   // cone rows: Qe(-E e_k)
+                if constexpr (!BALL) {
+                    const double zc = (g.kind == SOC_CONE) ? ze : 0.0;   // cone rows: Qe(-E e_k)
 #pragma unroll
-                for (int c = 0; c < 3; ++c) g.u[c] = fma(zc, G[OR + 4 * b + e][c], g.u[c]);
+                    for (int c = 0; c < 3; ++c) g.u[c] = fma(zc, G[OR + 4 * b + e][c], g.u[c]);
+                }
             }
         }
 #pragma unroll
@@ -1233,9 +1335,10 @@ DCOL_HD void launder(P& p) {
 #endif
 }
 
-// FULL: every pair of the launch has o == OMAX (no padding rows; the host picks the
-// variant per launch, dcol_capi.cpp: bucket_pairs)
-template <int N, int NSOC, int OMAX, int LPP, bool FULL = false>
+// FULL: every pair of the launch has o == OMAX (no padding rows); BALL: every SOC block of
+// the launch is a ball block (Solver).  The host picks the variant per launch
+// (dcol_capi.cpp: bucket_pairs).
+template <int N, int NSOC, int OMAX, int LPP, bool FULL = false, bool BALL = false>
 DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
     DCOL_STAMP(A, pi, q, 0);
     const int64_t B = A.B;
@@ -1253,7 +1356,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
     make_frame(S2, th2, F2);
     DCOL_STAMP(A, pi, q, 1);
 
-    Solver<N, NSOC, OMAX, LPP> P;
+    Solver<N, NSOC, OMAX, LPP, BALL> P;
     P.q = q;
 #ifdef DCOL_STAMPS
     P.dbg = (q == 0) ? A.stamps + 16 * pi + 8 : nullptr;
@@ -1294,7 +1397,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
             // lane differentiates one primitive: lane q takes primitive q & 1, so a 2+-lane
             // group does the two 6-coordinate gradients side by side instead of both in
             // every lane (a 1-lane group does both in turn)
-            using Agg = typename Solver<N, NSOC, OMAX, LPP>::LagAgg;
+            using Agg = typename Solver<N, NSOC, OMAX, LPP, BALL>::LagAgg;
             const Agg ag0 = P.lag_aggregate(T1, 0);
             const Agg ag1 = P.lag_aggregate(T2, 1);
             constexpr int NP = LPP >= 2 ? 1 : 2;
@@ -1355,14 +1458,15 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
 constexpr int kSolveBlock = DCOL_BLOCK;
 static_assert(kSolveBlock % 64 == 0, "one or more whole waves per workgroup");
 
-template <int N, int NSOC, int OMAX, int LPP, int WPS, bool FULL>
+// FL: variant flags, bit 0 FULL, bit 1 BALL (variants.py)
+template <int N, int NSOC, int OMAX, int LPP, int WPS, int FL>
 __global__ void __launch_bounds__(kSolveBlock, WPS) prox_kernel(KArgs A) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t slot = t / LPP;
     const int q = (int)(t % LPP);
     if (slot >= A.n) return;
     const int64_t pi = A.perm ? (int64_t)A.perm[A.slot0 + slot] : (A.slot0 + slot);
-    solve_one<N, NSOC, OMAX, LPP, FULL>(A, pi, q);
+    solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0>(A, pi, q);
 }
 
 }  // namespace dcol

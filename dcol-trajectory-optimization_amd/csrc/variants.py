@@ -20,6 +20,11 @@ polytope-polytope pairs) runs a copy of the kernel with the padding masks folded
 Built for the polytope x polytope shapes (the only ones whose row count commonly fills
 its bucket; a SOC pair's 1-row cone base or sphere's 0 rows never does).
 
+BALL variants: a launch whose SOC blocks are all ball blocks (sphere / capsule / cylinder /
+polygon -- no cone) runs a copy of the kernel that holds those blocks in structured form
+(radius + extra columns instead of 4 dense G rows; dcol_device.hpp Solver<..., BALL>).
+Built for every SOC shape with N <= 6; the host buckets cone pairs apart.
+
 FUSED variants: one launch for a whole small plan.  A plan that mixes several variants
 and cannot fill the GPU (an ALTRO phase: one victim against spheres, capsules, cylinders,
 cones and polytopes) runs every bucket in ONE launch of prox_fused_kernel, whose
@@ -27,11 +32,12 @@ workgroups switch on a per-segment variant id (dcol_kernels_fused.hip) — no st
 one launch latency.  Each shape's latency configuration (largest LPP) is in the switch,
 plus the padding-free copies of the FULL shapes; case-4 shapes (N = 7, 8) are not.
 
-Generates dcol_variants.inc:
+Generates dcol_variants.inc (FL = variant flags: bit 0 FULL, bit 1 BALL):
   DCOL_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, 0) for every compiled kernel
   DCOL_FULL_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, 1) for the padding-free copies
+  DCOL_BALL_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, 2) for the ball-SOC copies
   DCOL_SHAPES(X)    X(N, NSOC, OMAX) once per shape (used by the test emulator)
-  DCOL_FUSED_VARIANTS(X)  X(ID, N, NSOC, OMAX, LPP, FULL) the cases of the fused kernel
+  DCOL_FUSED_VARIANTS(X)  X(ID, N, NSOC, OMAX, LPP, FL) the cases of the fused kernel
 """
 import os
 
@@ -70,6 +76,11 @@ CONFIG = {
     (6, 2, 8): [(2, 1), (8, 1)],
 }
 FULL = {(4, 0)}   # shapes with padding-free copies (see module docstring)
+
+
+def ball(n, nsoc):
+    """shapes with ball-SOC copies (see module docstring)"""
+    return nsoc >= 1 and n <= 6
 BIG = 24   # OMAX >= BIG with SOC blocks: 8 lanes per pair
 
 
@@ -91,6 +102,8 @@ def fused():
             out.append((n, s, o, lpp, 0))
             if (n, s) in FULL:
                 out.append((n, s, o, lpp, 1))
+            if ball(n, s):
+                out.append((n, s, o, lpp, 2))
     return out
 
 
@@ -101,6 +114,8 @@ def main():
     lines += [f"    X({n}, {s}, {o}, {l}, {w}, 0) \\" for n, s, o in shapes for l, w in configs(n, s, o)]
     lines += ["", "#define DCOL_FULL_VARIANTS(X) \\"]
     lines += [f"    X({n}, {s}, {o}, {l}, {w}, 1) \\" for n, s, o in shapes if (n, s) in FULL for l, w in configs(n, s, o)]
+    lines += ["", "#define DCOL_BALL_VARIANTS(X) \\"]
+    lines += [f"    X({n}, {s}, {o}, {l}, {w}, 2) \\" for n, s, o in shapes if ball(n, s) for l, w in configs(n, s, o)]
     lines += ["", "#define DCOL_SHAPES(X) \\"]
     lines += [f"    X({n}, {s}, {o}) \\" for n, s, o in shapes]
     lines += ["", "#define DCOL_FUSED_VARIANTS(X) \\"]

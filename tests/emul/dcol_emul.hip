@@ -45,6 +45,7 @@ extern "C" int dcol_emul_batch(const dcol_shape_desc* shapes, int32_t n, int64_t
     A.grad = gr.data();
     A.iters = iters;
     A.status = status;
+    const bool no_ball = std::getenv("DCOL_NO_BALL") != nullptr;
     for (int64_t i = 0; i < B; ++i) {
         PairClass c = classify(sh[s1[i]], sh[s2[i]]);
         if (c.status != DCOL_OK) {
@@ -56,11 +57,19 @@ extern "C" int dcol_emul_batch(const dcol_shape_desc* shapes, int32_t n, int64_t
             continue;
         }
         const bool full = c.o == c.omax;   // both loop specialisations, as the GPU launches pick them
+        // ball-SOC specialisation as the GPU plans pick it (DCOL_NO_BALL: the dense rows)
+        const bool ball = c.nsoc > 0 && sh[s1[i]].soc_kind != SOC_CONE && sh[s2[i]].soc_kind != SOC_CONE && !no_ball;
 #define DCOL_EMUL(NN, NS, OM)                                                    \
         if (c.N == NN && c.nsoc == NS && c.omax == OM) {                         \
             if constexpr (NN == 4 && NS == 0) {   /* variants.py FULL shapes */  \
                 if (full) {                                                      \
                     solve_one<NN, NS, OM, 1, true>(A, i, 0);                     \
+                    continue;                                                    \
+                }                                                                \
+            }                                                                    \
+            if constexpr (NS > 0 && NN <= 6) {    /* variants.py ball() */       \
+                if (ball) {                                                      \
+                    solve_one<NN, NS, OM, 1, false, true>(A, i, 0);              \
                     continue;                                                    \
                 }                                                                \
             }                                                                    \

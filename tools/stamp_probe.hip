@@ -95,7 +95,7 @@ int main(int argc, char** argv) {
     constexpr int LPP = 2;
     const int64_t grid = (B * LPP + kSolveBlock - 1) / kSolveBlock;
     for (int rep = 0; rep < 3; ++rep) {
-        hipLaunchKernelGGL((prox_kernel<4, 0, 12, LPP, 2, true>), dim3(grid), dim3(kSolveBlock), 0, 0, a);
+        hipLaunchKernelGGL((prox_kernel<4, 0, 12, LPP, 2, 1>), dim3(grid), dim3(kSolveBlock), 0, 0, a);
         CK(hipDeviceSynchronize());
     }
     std::vector<unsigned long long> st(16 * B);
