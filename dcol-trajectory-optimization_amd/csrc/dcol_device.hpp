@@ -282,8 +282,18 @@ DCOL_HD void soc_nt(const double* s, const double* z, SocNT& W) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) W.w1[k] = (sb[k + 1] - zb[k + 1]) * i2g;
     W.bf = frcp(W.w0 + 1.0);
+#if defined(__HIP_DEVICE_COMPILE__)
+    // eta = (J(s)/J(z))^(1/4) = sqrt(u), u = sqrt(J(s)) / sqrt(J(z)) = J(s) is iz from the
+    // normalisations above: one reciprocal square root instead of two sqrt sequences and two
+    // reciprocals (rounding-level)
+    const double u = (Js * is) * iz;
+    const double ie = frsqrt(u);
+    W.eta = (Jz != 0.0) ? u * ie : 1.0;                     // quirk Q9
+    W.ieta = (Jz != 0.0) ? ie : 1.0;
+#else
     W.eta = (Jz != 0.0) ? sqrt(sqrt(Js * frcp(Jz))) : 1.0;   // quirk Q9
     W.ieta = frcp(W.eta);
+#endif
 }
 
 // out = W v
@@ -338,8 +348,11 @@ DCOL_HD void soc_iprod(const double* u, const double* w, double* out) {
     for (int k = 1; k < 4; ++k) out[k] = irho * (c1 * u[k] + c2 * w[k]);
 }
 
-// soc_linesearch, pdip.py:25-52 (quirk Q10: nu floored at 1e-25)
-DCOL_HD double soc_ls(const double* y, const double* d) {
+// soc_linesearch, pdip.py:25-52 (quirk Q10: nu floored at 1e-25), in inverse form: returns
+// 1 / step bound = max(1, |rho_1| - rho_0) (the reference's min(1, 1/(|rho_1| - rho_0)) if
+// |rho_1| > rho_0, else 1), so the caller takes one reciprocal of the combined orthant /
+// SOC maximum (bound_inv) instead of one per cone.
+DCOL_HD double soc_ls_inv(const double* y, const double* d) {
     const double nu = fmax(y[0] * y[0] - (y[1] * y[1] + y[2] * y[2] + y[3] * y[3]), 1e-25);
     const double zeta = y[0] * d[0] - (y[1] * d[1] + y[2] * d[2] + y[3] * d[3]);
     const double isn = frsqrt(nu);
@@ -352,8 +365,12 @@ DCOL_HD double soc_ls(const double* y, const double* d) {
         const double r = d[k] * isn - coef * (y[k] * inu);
         n2 += r * r;
     }
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double n1 = n2 > 0.0 ? n2 * frsqrt(n2) : 0.0;   // |rho_1| without the sqrt sequence
+#else
     const double n1 = sqrt(n2);
-    return (n1 > rho0) ? fmin(1.0, frcp(n1 - rho0)) : 1.0;
+#endif
+    return fmax(1.0, n1 - rho0);                          // NaN -> 1, as the reference's test
 }
 
 // ------------------------------------------------------------------------------------
@@ -959,10 +976,10 @@ struct Solver {
             double cp[M];                                // (W^-1 ds_a) o (W dz_a)
             double dsS[SSA * 4], dzS[SSA * 4];           // SOC rows of the affine step
             double dx[N];
-            double cmax = 1.0, als = 1.0, p1 = 0.0, p2 = 0.0;
+            double cmax = 1.0, p1 = 0.0, p2 = 0.0;
             predictor<FULL>(so, il, F, idg, rx, dx, cp, dsS, dzS, cmax, p1, p2);
-            soc_bound(dsS, dzS, als);
-            const double aa = R::min(fmin(frcp(cmax), als));        // quirk Q5 (no 0.99)
+            soc_bound(dsS, dzS, cmax);
+            const double aa = frcp(R::max(cmax));                   // quirk Q5 (no 0.99)
             DCOL_ISTAMP(it, 3);
             // rho = (s + aa ds)'(z + aa dz) / s'z, expanded as
             // s'z + aa (s'dz + z'ds) + aa^2 ds'dz (orthant sums accumulated by predictor())
@@ -994,7 +1011,7 @@ struct Solver {
             DCOL_ISTAMP(it, 4);
             rhs_solve(so, il, F, idg, rx, cp, smu, dx, sbzt, slds);
             DCOL_ISTAMP(it, 5);
-            cmax = 1.0; als = 1.0;
+            cmax = 1.0;
             double cu[OR > 0 ? OR : 1], cdz[OR > 0 ? OR : 1];   // G dx and dz, kept for the update
 #pragma unroll
             for (int k = 0; k < OR; ++k) {
@@ -1008,10 +1025,10 @@ struct Solver {
             for (int b = 0; b < SS; ++b) {
                 soc_step(so[b], OR + 4 * b, sbzt[b], slds[b], dx, su[b], sdz[b], sds[b]);
                 const int k0 = OR + 4 * b;
-                const double lb = fmin(soc_ls(s + k0, sds[b]), soc_ls(z + k0, sdz[b]));
-                als = vs[b] ? fmin(als, lb) : als;
+                const double ib = fmax(soc_ls_inv(s + k0, sds[b]), soc_ls_inv(z + k0, sdz[b]));
+                cmax = vs[b] ? fmax(cmax, ib) : cmax;
             }
-            const double a = fmin(1.0, 0.99 * R::min(fmin(frcp(cmax), als)));
+            const double a = fmin(1.0, 0.99 * frcp(R::max(cmax)));
             DCOL_ISTAMP(it, 6);
 #pragma unroll
             for (int j = 0; j < N; ++j) x[j] += a * dx[j];
@@ -1147,13 +1164,13 @@ struct Solver {
         soc_iprod(S.lam, v, out);
     }
     // SOC part of the step bound (soc_linesearch over the lane's blocks; ds/dz hold the
-    // SOC rows only)
-    DCOL_HD void soc_bound(const double* ds, const double* dz, double& als) const {
+    // SOC rows only), as a running max of inverse bounds like the orthant's cmax
+    DCOL_HD void soc_bound(const double* ds, const double* dz, double& cmax) const {
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
             const int k0 = OR + 4 * b;
-            const double lb = fmin(soc_ls(s + k0, ds + 4 * b), soc_ls(z + k0, dz + 4 * b));
-            als = vs[b] ? fmin(als, lb) : als;
+            const double ib = fmax(soc_ls_inv(s + k0, ds + 4 * b), soc_ls_inv(z + k0, dz + 4 * b));
+            cmax = vs[b] ? fmax(cmax, ib) : cmax;
         }
     }
 
