@@ -244,6 +244,25 @@ bool ball_disabled() {
     return off;
 }
 
+// A launch too small to fill the GPU runs the configuration with the shortest per-pair
+// latency: fewest orthant slots per lane (omax / lpp), over the pair's bucket and the larger
+// buckets up to twice its rows (a tight bucket compiled only with LPP 2 -- 6 or 10 rows --
+// loses to the next bucket's 8-lane groups), fewer rows on ties.
+void latency_config(Launch& L) {
+    int best_o = L.omax, best_l = max_lpp(L.N, L.nsoc, L.omax);
+    for (const int om : buckets().at({L.N, L.nsoc})) {
+        if (om <= L.omax || om > 2 * L.omax) continue;
+        const int l = max_lpp(L.N, L.nsoc, om);
+        if (om * best_l < best_o * l) {   // om / l < best_o / best_l
+            best_o = om;
+            best_l = l;
+        }
+    }
+    if (best_o != L.omax) L.full = false;   // the pairs no longer fill the bucket
+    L.omax = best_o;
+    L.lpp = best_l;
+}
+
 // Classify + bucket (counting sort by variant key).  Fills p->launches and the slot->pair
 // permutation; returns DCOL_SUCCESS or an error.
 int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, dcol_plan* p,
@@ -283,7 +302,7 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
         L.slot0 = (int64_t)perm.size();
         L.n = (int64_t)kv.second.size();
         if (L.kind == 0 && !lpp_forced() && L.n * L.lpp < 64LL * t->simds)   // cannot fill the GPU
-            L.lpp = max_lpp(L.N, L.nsoc, L.omax);
+            latency_config(L);
         perm.insert(perm.end(), kv.second.begin(), kv.second.end());
         p->launches.push_back(L);
     }

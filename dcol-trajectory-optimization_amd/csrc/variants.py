@@ -43,12 +43,12 @@ import os
 
 OMAX = {
     (4, 0): [4, 8, 12, 16, 24, 32],     # polytope x polytope
-    (4, 1): [2, 4, 8, 12, 16, 24, 32],  # polytope x {sphere, cone}
+    (4, 1): [2, 4, 6, 8, 12, 16, 24, 32],  # polytope x {sphere, cone}
     (4, 2): [2],                        # {sphere, cone} x {sphere, cone}
-    (5, 1): [8, 12, 16, 24, 32],        # {capsule, cylinder} x polytope
-    (5, 2): [2, 4, 8],                  # {capsule, cylinder} x {sphere, cone}
+    (5, 1): [8, 10, 12, 16, 24, 32],    # {capsule, cylinder} x polytope
+    (5, 2): [2, 4, 6, 8],               # {capsule, cylinder} x {sphere, cone}
     (6, 1): [8, 12, 16, 24, 32],        # polygon x polytope
-    (6, 2): [2, 4, 8, 12, 16, 24, 32],  # polygon x {sphere, cone}; case-4 {capsule, cylinder}^2
+    (6, 2): [2, 4, 6, 8, 12, 16, 24, 32],  # polygon x {sphere, cone}; case-4 {capsule, cylinder}^2
     (7, 2): [4, 8, 12, 16, 24, 32],     # case-4 extension: {capsule, cylinder} x polygon
     (8, 2): [4, 8, 12, 16, 24, 32],     # case-4 extension: polygon x polygon
 }
@@ -63,15 +63,20 @@ CONFIG = {
     (4, 0, 32): [(8, 2)],
     (4, 1, 2): [(2, 1)],
     (4, 1, 4): [(1, 1), (2, 2), (4, 2)],
+    (4, 1, 6): [(2, 2), (1, 1)],        # sphere x box: 2 waves/SIMD spill-free with ball rows
     (4, 1, 8): [(1, 1), (2, 1), (8, 2)],
     (4, 1, 12): [(2, 1), (4, 1)],
     (4, 2, 2): [(2, 2)],
     (5, 1, 8): [(1, 1), (2, 1), (8, 1)],
+    (5, 1, 10): [(2, 1)],               # cylinder x box
     (5, 1, 12): [(2, 1), (4, 1)],
     (5, 2, 2): [(2, 2)],
     (5, 2, 4): [(2, 1), (4, 1)],
+    (5, 2, 6): [(2, 1)],
     (5, 2, 8): [(2, 1), (8, 1)],
     (6, 1, 8): [(2, 1), (8, 1)],
+    (6, 1, 12): [(2, 1), (4, 1)],       # polygon x box: LPP 2 measured +22 % over 4
+    (6, 2, 6): [(2, 1)],
     (6, 2, 4): [(2, 1), (4, 1)],
     (6, 2, 8): [(2, 1), (8, 1)],
 }
