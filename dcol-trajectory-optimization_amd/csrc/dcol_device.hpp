@@ -261,6 +261,10 @@ DCOL_HD void dcm_jacobian(const double p[3], double dQ[3][9]) {
 // ------------------------------------------------------------------------------------
 struct SocNT {
     double w0, w1[3], bf, eta, ieta;
+    // soc_linesearch inputs that depend only on the current s (index 0) / z (index 1), shared
+    // by the predictor's and the corrector's line search: 1/sqrt(max(J, 1e-25)) and
+    // 1/(y_0 / sqrt(nu) + 1)
+    double lis[2], lrc[2];
 };
 
 // soc_NT_scaling, NT_scaling.py:340-405; W = eta * Wbar,
@@ -282,6 +286,17 @@ DCOL_HD void soc_nt(const double* s, const double* z, SocNT& W) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) W.w1[k] = (sb[k + 1] - zb[k + 1]) * i2g;
     W.bf = frcp(W.w0 + 1.0);
+#if defined(__HIP_DEVICE_COMPILE__)
+    // line-search scalars from the normalisation rsqrts (same J expressions as soc_ls_inv);
+    // J below the reference's 1e-25 floor (or NaN) takes 1/sqrt(1e-25)
+    W.lis[0] = (Js >= 1e-25) ? is : 3162277660168.3794;
+    W.lis[1] = (Jz >= 1e-25) ? iz : 3162277660168.3794;
+#else
+    W.lis[0] = frsqrt(fmax(Js, 1e-25));
+    W.lis[1] = frsqrt(fmax(Jz, 1e-25));
+#endif
+    W.lrc[0] = frcp(fma(s[0], W.lis[0], 1.0));
+    W.lrc[1] = frcp(fma(z[0], W.lis[1], 1.0));
 #if defined(__HIP_DEVICE_COMPILE__)
     // eta = (J(s)/J(z))^(1/4) = sqrt(u), u = sqrt(J(s)) / sqrt(J(z)) = J(s) is iz from the
     // normalisations above: one reciprocal square root instead of two sqrt sequences and two
@@ -352,13 +367,12 @@ DCOL_HD void soc_iprod(const double* u, const double* w, double* out) {
 // 1 / step bound = max(1, |rho_1| - rho_0) (the reference's min(1, 1/(|rho_1| - rho_0)) if
 // |rho_1| > rho_0, else 1), so the caller takes one reciprocal of the combined orthant /
 // SOC maximum (bound_inv) instead of one per cone.
-DCOL_HD double soc_ls_inv(const double* y, const double* d) {
-    const double nu = fmax(y[0] * y[0] - (y[1] * y[1] + y[2] * y[2] + y[3] * y[3]), 1e-25);
+// isn = 1/sqrt(nu), rc = 1/(y_0 isn + 1) come precomputed from soc_nt (SocNT::lis, lrc).
+DCOL_HD double soc_ls_inv(const double* y, const double* d, double isn, double rc) {
     const double zeta = y[0] * d[0] - (y[1] * d[1] + y[2] * d[2] + y[3] * d[3]);
-    const double isn = frsqrt(nu);
     const double inu = isn * isn;
     const double rho0 = zeta * inu;
-    const double coef = (zeta * isn + d[0]) * frcp(y[0] * isn + 1.0);
+    const double coef = (zeta * isn + d[0]) * rc;
     double n2 = 0.0;
 #pragma unroll
     for (int k = 1; k < 4; ++k) {
@@ -978,7 +992,7 @@ struct Solver {
             double dx[N];
             double cmax = 1.0, p1 = 0.0, p2 = 0.0;
             predictor<FULL>(so, il, F, idg, rx, dx, cp, dsS, dzS, cmax, p1, p2);
-            soc_bound(dsS, dzS, cmax);
+            soc_bound(so, dsS, dzS, cmax);
             const double aa = frcp(R::max(cmax));                   // quirk Q5 (no 0.99)
             DCOL_ISTAMP(it, 3);
             // rho = (s + aa ds)'(z + aa dz) / s'z, expanded as
@@ -1024,9 +1038,7 @@ struct Solver {
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
                 soc_step(so[b], OR + 4 * b, sbzt[b], slds[b], dx, su[b], sdz[b], sds[b]);
-                const int k0 = OR + 4 * b;
-                const double ib = fmax(soc_ls_inv(s + k0, sds[b]), soc_ls_inv(z + k0, sdz[b]));
-                cmax = vs[b] ? fmax(cmax, ib) : cmax;
+                cmax = soc_bound1(so[b].W, b, sds[b], sdz[b], cmax);
             }
             const double a = fmin(1.0, 0.99 * frcp(R::max(cmax)));
             DCOL_ISTAMP(it, 6);
@@ -1165,13 +1177,14 @@ struct Solver {
     }
     // SOC part of the step bound (soc_linesearch over the lane's blocks; ds/dz hold the
     // SOC rows only), as a running max of inverse bounds like the orthant's cmax
-    DCOL_HD void soc_bound(const double* ds, const double* dz, double& cmax) const {
+    DCOL_HD void soc_bound(const SocState* so, const double* ds, const double* dz, double& cmax) const {
 #pragma unroll
-        for (int b = 0; b < SS; ++b) {
-            const int k0 = OR + 4 * b;
-            const double ib = fmax(soc_ls_inv(s + k0, ds + 4 * b), soc_ls_inv(z + k0, dz + 4 * b));
-            cmax = vs[b] ? fmax(cmax, ib) : cmax;
-        }
+        for (int b = 0; b < SS; ++b) cmax = soc_bound1(so[b].W, b, ds + 4 * b, dz + 4 * b, cmax);
+    }
+    DCOL_HD double soc_bound1(const SocNT& W, int b, const double* ds, const double* dz, double cmax) const {
+        const int k0 = OR + 4 * b;
+        const double ib = fmax(soc_ls_inv(s + k0, ds, W.lis[0], W.lrc[0]), soc_ls_inv(z + k0, dz, W.lis[1], W.lrc[1]));
+        return vs[b] ? fmax(cmax, ib) : cmax;
     }
 
     // -------- gradient helpers ---------------------------------------------------------

@@ -75,7 +75,7 @@ CONFIG = {
     (5, 2, 6): [(2, 1)],
     (5, 2, 8): [(2, 1), (8, 1)],
     (6, 1, 8): [(2, 1), (8, 1)],
-    (6, 1, 12): [(2, 1), (4, 1)],       # polygon x box: LPP 2 measured +22 % over 4
+    (6, 1, 12): [(4, 1), (2, 1)],       # polygon x box (ball rows; LPP 2 only dense, BALL_SKIP)
     (6, 2, 6): [(2, 1)],
     (6, 2, 4): [(2, 1), (4, 1)],
     (6, 2, 8): [(2, 1), (8, 1)],
@@ -86,6 +86,15 @@ FULL = {(4, 0)}   # shapes with padding-free copies (see module docstring)
 def ball(n, nsoc):
     """shapes with ball-SOC copies (see module docstring)"""
     return nsoc >= 1 and n <= 6
+
+
+# (N, NSOC, OMAX, LPP) configurations without a ball copy: (6, 1, 12) at LPP 2 is the one
+# ball kernel that spills to scratch (36 B/lane); as the throughput choice its alpha drifted
+# to 3e-10 rel of the C oracle (gradients 2e-5) on the mixed 1M workload, against <= 6e-12
+# for every other variant (tests/test_gpu_fullsize.py checks all throughput variants
+# against the oracle).  Polygon x box runs the ball rows at LPP 4 (3.4e8 pair-solves/s;
+# the dense rows at LPP 2: 2.9e8).
+BALL_SKIP = {(6, 1, 12, 2)}
 BIG = 24   # OMAX >= BIG with SOC blocks: 8 lanes per pair
 
 
@@ -107,7 +116,7 @@ def fused():
             out.append((n, s, o, lpp, 0))
             if (n, s) in FULL:
                 out.append((n, s, o, lpp, 1))
-            if ball(n, s):
+            if ball(n, s) and (n, s, o, lpp) not in BALL_SKIP:
                 out.append((n, s, o, lpp, 2))
     return out
 
@@ -120,7 +129,8 @@ def main():
     lines += ["", "#define DCOL_FULL_VARIANTS(X) \\"]
     lines += [f"    X({n}, {s}, {o}, {l}, {w}, 1) \\" for n, s, o in shapes if (n, s) in FULL for l, w in configs(n, s, o)]
     lines += ["", "#define DCOL_BALL_VARIANTS(X) \\"]
-    lines += [f"    X({n}, {s}, {o}, {l}, {w}, 2) \\" for n, s, o in shapes if ball(n, s) for l, w in configs(n, s, o)]
+    lines += [f"    X({n}, {s}, {o}, {l}, {w}, 2) \\" for n, s, o in shapes if ball(n, s) for l, w in configs(n, s, o)
+              if (n, s, o, l) not in BALL_SKIP]
     lines += ["", "#define DCOL_SHAPES(X) \\"]
     lines += [f"    X({n}, {s}, {o}) \\" for n, s, o in shapes]
     lines += ["", "#define DCOL_FUSED_VARIANTS(X) \\"]
