@@ -929,23 +929,18 @@ struct Solver {
             }
             // ---- NT scalings, residuals, normal matrix (pdip.py:410-434)
             SocState so[SSA];
-            double rx[N], Hm[N][N];
+            double Hm[N][N];
 #pragma unroll
-            for (int j = 0; j < N; ++j) {
-                rx[j] = 0.0;
+            for (int j = 0; j < N; ++j)
 #pragma unroll
                 for (int c = j; c < N; ++c) Hm[j][c] = 0.0;
-            }
 #pragma unroll
             for (int k = 0; k < OR; ++k) {
                 const double zk = z[k];
                 const double d = zk * il[k];              // W^-2 = z / s on the orthant
                 double g[N];
 #pragma unroll
-                for (int j = 0; j < N; ++j) {
-                    rx[j] += G[k][j] * zk;
-                    g[j] = G[k][j] * d;
-                }
+                for (int j = 0; j < N; ++j) g[j] = G[k][j] * d;
 #pragma unroll
                 for (int j = 0; j < N; ++j)
 #pragma unroll
@@ -957,7 +952,6 @@ struct Solver {
                 soc_nt(s + k0, z + k0, so[b].W);
                 soc_mul(so[b].W, z + k0, so[b].lam);
                 soc_prod(so[b].lam, so[b].lam, so[b].ll);
-                soc_gtv(b, z + k0, rx);
             }
             // SOC part of the normal matrix
 #pragma unroll
@@ -971,8 +965,7 @@ struct Solver {
 #pragma unroll
                         for (int c = j; c < N; ++c) Hm[j][c] += gt[e][j] * gt[e][c];
             }
-            allsum_sym(Hm);                                 // rx stays lane-partial: it is reduced
-                                                            // inside each right-hand side
+            allsum_sym(Hm);
             DCOL_ISTAMP(it, 1);
             double F[N][N], idg[N];
             if (!chol(Hm, F, idg)) {                        // scipy check_finite -> ValueError,
@@ -991,7 +984,7 @@ struct Solver {
             double dsS[SSA * 4], dzS[SSA * 4];           // SOC rows of the affine step
             double dx[N];
             double cmax = 1.0, p1 = 0.0, p2 = 0.0;
-            predictor<FULL>(so, il, F, idg, rx, dx, cp, dsS, dzS, cmax, p1, p2);
+            predictor<FULL>(so, il, F, idg, dx, cp, dsS, dzS, cmax, p1, p2);
             soc_bound(so, dsS, dzS, cmax);
             const double aa = frcp(R::max(cmax));                   // quirk Q5 (no 0.99)
             DCOL_ISTAMP(it, 3);
@@ -1023,7 +1016,7 @@ struct Solver {
             const double smu = sigma * mu;
             double sbzt[SSA][4], slds[SSA][4];
             DCOL_ISTAMP(it, 4);
-            rhs_solve(so, il, F, idg, rx, cp, smu, dx, sbzt, slds);
+            rhs_solve(so, il, F, idg, cp, smu, dx, sbzt, slds);
             DCOL_ISTAMP(it, 5);
             cmax = 1.0;
             double cu[OR > 0 ? OR : 1], cdz[OR > 0 ? OR : 1];   // G dx and dz, kept for the update
@@ -1072,15 +1065,17 @@ struct Solver {
     // Corrector: lambda\ds = lambda\(-lambda o lambda - cp + smu e).  Then
     // b~z = W^-1(-rz - W lds); dx = (G~'G~)^-1(-rx + G' W^-1 b~z);
     // dz = W^-1(W^-1 G dx - b~z); ds = W(lds - W dz)          (pdip.py:424-460)
+    // rx = G'z + c is folded into the same row sums: -rx + G'(W^-1 b~z) = G'(W^-1 b~z - z) - c,
+    // and on an orthant row (W^-1 b~z)_k - z_k = -(z (s + r) + smu - cp) / s  (one G'v pass
+    // per right-hand side, no separate G'z accumulation).
     DCOL_HD void rhs_solve(const SocState* so, const double* il, const double (&F)[N][N], const double (&idg)[N],
-                           const double* rx, const double* cp, double smu, double* dx, double (*sbzt)[4],
-                           double (*slds)[4]) const {
+                           const double* cp, double smu, double* dx, double (*sbzt)[4], double (*slds)[4]) const {
         double rhs[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) rhs[j] = 0.0;
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
-            const double t = -orth_num(k, cp, smu, r[k]) * il[k];    // (W^-1 b~z)_k
+            const double t = -orth_num(k, cp, smu, s[k] + r[k]) * il[k];   // (W^-1 b~z)_k - z_k
 #pragma unroll
             for (int j = 0; j < N; ++j) rhs[j] += G[k][j] * t;
         }
@@ -1096,10 +1091,11 @@ struct Solver {
             soc_w2inv(so[b].W, sr, q);
 #pragma unroll
             for (int e = 0; e < 4; ++e) sbzt[b][e] = -q[e] - m[e];
-            soc_gtv(b, sbzt[b], rhs);
-        }
+            double bz[4];
 #pragma unroll
-        for (int j = 0; j < N; ++j) rhs[j] -= rx[j];     // lane partials of G'z
+            for (int e = 0; e < 4; ++e) bz[e] = sbzt[b][e] - z[k0 + e];
+            soc_gtv(b, bz, rhs);
+        }
         allsum_vec(rhs);
         rhs[3] -= 1.0;                                   // - c (c = e_3)
         chol_solve(F, idg, rhs, dx);
@@ -1135,10 +1131,10 @@ struct Solver {
     // p1 = s'dz + z'ds, p2 = ds'dz that rho needs.  SOC rows keep ds/dz (dsS, dzS).
     template <bool FULL>
     DCOL_HD void predictor(const SocState* so, const double* il, const double (&F)[N][N], const double (&idg)[N],
-                           const double* rx, double* dx, double* cp, double* dsS, double* dzS, double& cmax,
+                           double* dx, double* cp, double* dsS, double* dzS, double& cmax,
                            double& p1, double& p2) const {
         double sbzt[SSA][4], slds[SSA][4];
-        rhs_solve(so, il, F, idg, rx, nullptr, 0.0, dx, sbzt, slds);
+        rhs_solve(so, il, F, idg, nullptr, 0.0, dx, sbzt, slds);
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
             const double u = rowdot(k, dx);
