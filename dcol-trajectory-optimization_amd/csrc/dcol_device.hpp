@@ -905,13 +905,13 @@ struct Solver {
             DCOL_ISTAMP(it, 0);
             // ---- mu = s'z / deg and the exit test first (pdip.py:410-422, quirk Q3): the
             // iteration that returns does not build the normal matrix
-            double il[OR > 0 ? OR : 1], iz[OR > 0 ? OR : 1];   // orthant rows: 1 / s, 1 / z
+            double il[OR > 0 ? OR : 1], isz[OR > 0 ? OR : 1];   // orthant rows: 1 / s, 1 / (s z)
             double sz = 0.0;
 #pragma unroll
             for (int k = 0; k < OR; ++k) {
                 const double rsz = frcp(s[k] * z[k]);   // one reciprocal for both
                 il[k] = z[k] * rsz;
-                iz[k] = s[k] * rsz;
+                isz[k] = rsz;
                 sz = fma(live<FULL>(k) ? s[k] : 0.0, z[k], sz);
             }
 #pragma unroll
@@ -1022,10 +1022,10 @@ struct Solver {
             double cu[OR > 0 ? OR : 1], cdz[OR > 0 ? OR : 1];   // G dx and dz, kept for the update
 #pragma unroll
             for (int k = 0; k < OR; ++k) {
-                double dsk;
-                orth_step(k, il, cp, smu, dx, cu[k], cdz[k], dsk);
+                double dsk, num;
+                orth_step(k, il, cp, smu, dx, cu[k], cdz[k], dsk, num);
                 cmax = bound_inv(cmax, dsk, il[k]);
-                cmax = bound_inv(cmax, cdz[k], iz[k]);
+                cmax = bound_inv(cmax, num, isz[k]);       // -dz / z = -num / (s z)
             }
             double sdz[SSA][4], sds[SSA][4], su[SSA][4];
 #pragma unroll
@@ -1105,9 +1105,10 @@ struct Solver {
     //   dz = (z (u + r) + smu - cp) / s,   ds = -(s + r) - u   (u = G_k dx, r = G_k x - h_k),
     // i.e. the primal and complementarity rows of the same Newton system, in fewer operations.
     DCOL_HD void orth_step(int k, const double* il, const double* cp, double smu, const double* dx, double& u,
-                           double& dz, double& ds) const {
+                           double& dz, double& ds, double& num) const {
         u = rowdot(k, dx);
-        dz = orth_num(k, cp, smu, u + r[k]) * il[k];
+        num = orth_num(k, cp, smu, u + r[k]);
+        dz = num * il[k];
         ds = -(s[k] + r[k]) - u;
     }
     // one SOC block of the step: dz = W^-1(W^-1 u - b~z) = W^-2 u - W^-1 b~z (wbz), and

@@ -8,7 +8,7 @@ NAME=${1:?name}
 OUT=gpurun_out/$NAME
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-B="python3 bench.py --no-cpu --no-altro --check 0 --steps 10 --warmup 2 --streams 1"
+B="python3 bench.py --no-cpu --no-altro --check 0 --steps 200 --warmup 100 --streams 1"
 tools/gpu_session.sh \
   "tests|600|python3 -m pytest tests -m gpu -q -x" \
   "bench_default|400|python3 bench.py" \
