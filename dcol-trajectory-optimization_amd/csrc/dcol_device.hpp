@@ -1041,18 +1041,21 @@ struct Solver {
             for (int k = 0; k < OR; ++k) {
                 const double dsk = -(s[k] + r[k]) - cu[k];
                 r[k] += a * cu[k];
-                const bool v = live<FULL>(k);
-                s[k] = v ? s[k] + a * dsk : s[k];
-                z[k] = v ? z[k] + a * cdz[k] : z[k];
+                // padding rows / inert SOC slots keep s = z = e: a zero step (their ds, dz
+                // are finite), one select per row instead of one per updated value
+                const double ak = live<FULL>(k) ? a : 0.0;
+                s[k] += ak * dsk;
+                z[k] += ak * cdz[k];
             }
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
                 const int k0 = OR + 4 * b;
+                const double ab = vs[b] ? a : 0.0;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     r[k0 + e] += a * su[b][e];
-                    s[k0 + e] = vs[b] ? s[k0 + e] + a * sds[b][e] : s[k0 + e];
-                    z[k0 + e] = vs[b] ? z[k0 + e] + a * sdz[b][e] : z[k0 + e];
+                    s[k0 + e] += ab * sds[b][e];
+                    z[k0 + e] += ab * sdz[b][e];
                 }
             }
             DCOL_ISTAMP(it, 7);
