@@ -215,6 +215,7 @@ def main():
         ev[k][1].record(stream)
     torch.cuda.synchronize(dev)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    e2e = end_to_end(args, eng, ids, s1, s2, p1, p2, pose1, pose2, out, step, dev) if world == 1 else None
     if dist is not None:
         t = torch.tensor([elapsed, kern_ms, elapsed_serial or 0.0], device=coll_dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -267,8 +268,11 @@ def main():
         "kernel_ms": kern_ms,
         "kernel_ms_max_rank": kern_ms_max,
         "solve_stats": {"ok_frac": float(np.mean(status == 0)), "iters_mean": float(iters[status == 0].mean()),
-                        "iters_max": int(iters.max())},
+                        "iters_max": int(iters.max()),
+                        "iters_hist": np.bincount(iters, minlength=int(iters.max()) + 1).tolist()},
     }
+    if e2e is not None:
+        line["end_to_end"] = e2e
     # spot parity check against the oracle on the first pairs of the timed batch
     if args.check and args.max_iter == 50:
         from oracle import dcol_oracle as O
@@ -290,6 +294,44 @@ def main():
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def end_to_end(args, eng, ids, s1, s2, p1, p2, pose1, pose2, out, step, dev, reps=20):
+    """The same batch with the poses starting in host memory (PCIe-inclusive; never `value`):
+    (a) pinned host poses -> H2D, the solve, D2H of alpha / grad / status / iters, on the
+    bench stream; (b) the C-ABI host call dcol_prox_batch_host (Engine.solve_host: pageable
+    numpy in/out, its own staging).  Median over reps, after one warm-up each."""
+    import torch
+    B = len(s1)
+    h1 = torch.from_numpy(np.ascontiguousarray(p1.T)).pin_memory()
+    h2 = torch.from_numpy(np.ascontiguousarray(p2.T)).pin_memory()
+    ho = {k: torch.empty(v.shape, dtype=v.dtype).pin_memory() for k, v in out.items()}
+
+    def pinned():
+        pose1.copy_(h1, non_blocking=True)
+        pose2.copy_(h2, non_blocking=True)
+        step()
+        for k, v in ho.items():
+            v.copy_(out[k], non_blocking=True)
+        torch.cuda.synchronize(dev)
+
+    def host():
+        eng.solve_host(ids[s1], ids[s2], p1, p2, grad=args.grad, contact=False)
+
+    res = {}
+    for name, fn in (("pinned_h2d_solve_d2h", pinned), ("solve_host_pageable", host)):
+        fn()
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        ms = 1e3 * float(np.median(ts))
+        res[name] = {"ms": ms, "pair_solves_per_s": B / (ms * 1e-3)}
+    res["bytes_h2d"] = int(2 * 48 * B)
+    res["bytes_d2h"] = int(sum(v.numel() * v.element_size() for v in ho.values()))
+    return res
 
 
 MIXED_KINDS = (0, 1, 2, 3, 4, 5)      # polytope sphere cone capsule cylinder polygon

@@ -19,6 +19,7 @@
 #include <mutex>
 #include <string>
 #include <tuple>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/dcol.h"
@@ -76,10 +77,12 @@ struct dcol_table {
     std::vector<DevRow> rows;
     DevShape* d_shapes = nullptr;
     DevRow* d_rows = nullptr;
-    // staging for dcol_prox_batch_host
+    // staging for dcol_prox_batch_host: device buffer + pinned host buffer (grow-only)
     std::mutex mu;
     void* stage = nullptr;
     size_t stage_bytes = 0;
+    void* hstage = nullptr;
+    size_t hstage_bytes = 0;
     int simds = 1024;   // SIMDs of the device (CUs x 4): below one wave per SIMD a launch is latency-bound
     // side streams for the concurrent variant launches of mixed plans (created on first use)
     std::mutex side_mu;
@@ -205,6 +208,7 @@ int dcol_table_destroy(dcol_table* t) {
     if (t->d_shapes) (void)hipFree(t->d_shapes);
     if (t->d_rows) (void)hipFree(t->d_rows);
     if (t->stage) (void)hipFree(t->stage);
+    if (t->hstage) (void)hipHostFree(t->hstage);
     if (t->side_ready)
         for (hipStream_t s : t->side) (void)hipStreamDestroy(s);
     delete t;
@@ -265,47 +269,79 @@ void latency_config(Launch& L) {
 
 // Classify + bucket (counting sort by variant key).  Fills p->launches and the slot->pair
 // permutation; returns DCOL_SUCCESS or an error.
+// O(B): each distinct (shape1, shape2) is classified once (a dense S x S cache for tables of
+// up to 2048 shapes, a hash map beyond), then a stable counting sort by group, groups in key
+// order.
 int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, dcol_plan* p,
                  std::vector<int32_t>& perm, bool case4) {
     const int32_t ns = (int32_t)t->shapes.size();
     // kind, N, nsoc, omax, lpp, ball (SOC blocks all balls: no cone), code
     using Key = std::tuple<int, int, int, int, int, int, int>;
-    std::map<Key, std::vector<int32_t>> groups;
-    std::map<Key, bool> full;
-    for (int64_t i = 0; i < B; ++i) {
-        if (s1[i] < 0 || s1[i] >= ns || s2[i] < 0 || s2[i] >= ns)
-            return fail(DCOL_ERR_ARG, "shape id out of range at pair " + std::to_string(i));
-        const DevShape& a = t->shapes[s1[i]];
-        const DevShape& b = t->shapes[s2[i]];
+    struct Group {
+        Key key;
+        bool full = true;   // every pair class of the group has o == omax
+        int64_t n = 0, at = 0;
+    };
+    std::map<Key, int32_t> gid_of_key;
+    std::vector<Group> groups;
+    auto classify_pair = [&](int32_t i1, int32_t i2) -> int32_t {
+        const DevShape& a = t->shapes[i1];
+        const DevShape& b = t->shapes[i2];
         PairClass c = classify(a, b, case4);
         const int ball = (c.nsoc > 0 && a.soc_kind != SOC_CONE && b.soc_kind != SOC_CONE && !ball_disabled()) ? 1 : 0;
         Key k = c.status == DCOL_OK ? Key{0, c.N, c.nsoc, c.omax, c.lpp, ball, 0} : Key{1, 0, 0, 0, 0, 0, c.status};
-        groups[k].push_back((int32_t)i);
-        auto f = full.emplace(k, true).first;
-        f->second = f->second && c.o == c.omax;
+        auto it = gid_of_key.emplace(k, (int32_t)groups.size()).first;
+        if (it->second == (int32_t)groups.size()) groups.push_back(Group{k});
+        Group& g = groups[it->second];
+        g.full = g.full && c.o == c.omax;
+        return it->second;
+    };
+    const bool dense = (int64_t)ns * ns <= (int64_t)1 << 22;
+    std::vector<int32_t> cache(dense ? (size_t)ns * ns : 0, -1);
+    std::unordered_map<int64_t, int32_t> sparse;
+    std::vector<int32_t> gid((size_t)B);
+    for (int64_t i = 0; i < B; ++i) {
+        const int32_t i1 = s1[i], i2 = s2[i];
+        if (i1 < 0 || i1 >= ns || i2 < 0 || i2 >= ns)
+            return fail(DCOL_ERR_ARG, "shape id out of range at pair " + std::to_string(i));
+        int32_t g;
+        if (dense) {
+            int32_t& e = cache[(size_t)i1 * ns + i2];
+            if (e < 0) e = classify_pair(i1, i2);
+            g = e;
+        } else {
+            auto it = sparse.find((int64_t)i1 * ns + i2);
+            if (it == sparse.end()) it = sparse.emplace((int64_t)i1 * ns + i2, classify_pair(i1, i2)).first;
+            g = it->second;
+        }
+        gid[i] = g;
+        ++groups[g].n;
     }
     p->table = t;
     p->B = B;
     p->launches.clear();
-    perm.clear();
-    perm.reserve(B);
-    for (auto& kv : groups) {
+    perm.assign((size_t)B, 0);
+    int64_t at = 0;
+    for (auto& kv : gid_of_key) {   // key order
+        Group& G = groups[kv.second];
+        G.at = at;
         Launch L;
-        L.kind = std::get<0>(kv.first);
-        L.N = std::get<1>(kv.first);
-        L.nsoc = std::get<2>(kv.first);
-        L.omax = std::get<3>(kv.first);
-        L.lpp = std::get<4>(kv.first);
-        L.code = std::get<6>(kv.first);
-        L.full = L.kind == 0 && full[kv.first];
-        L.ball = L.kind == 0 && std::get<5>(kv.first) == 1;
-        L.slot0 = (int64_t)perm.size();
-        L.n = (int64_t)kv.second.size();
+        L.kind = std::get<0>(G.key);
+        L.N = std::get<1>(G.key);
+        L.nsoc = std::get<2>(G.key);
+        L.omax = std::get<3>(G.key);
+        L.lpp = std::get<4>(G.key);
+        L.code = std::get<6>(G.key);
+        L.full = L.kind == 0 && G.full;
+        L.ball = L.kind == 0 && std::get<5>(G.key) == 1;
+        L.slot0 = at;
+        L.n = G.n;
         if (L.kind == 0 && !lpp_forced() && L.n * L.lpp < 64LL * t->simds)   // cannot fill the GPU
             latency_config(L);
-        perm.insert(perm.end(), kv.second.begin(), kv.second.end());
+        at += G.n;
         p->launches.push_back(L);
     }
+    for (int64_t i = 0; i < B; ++i) perm[(size_t)groups[gid[i]].at++] = (int32_t)i;   // stable
     assign_lanes(p);
     return DCOL_SUCCESS;
 }
@@ -581,29 +617,41 @@ int dcol_prox_batch_host(const dcol_table* tc, int64_t B, const int32_t* s1, con
     p.d_perm = p.launches.size() > 1 ? ib + 2 * B : nullptr;
     int32_t* dit = ib + 3 * B;
     int32_t* dst = ib + 4 * B;
-    // one H2D copy: [pose1 soa | pose2 soa] then [s1 | s2 | perm]
-    std::vector<double> soa(nin);
+    // pinned host staging (DMA at full link rate): [pose soa (12B) | outputs (16B)] doubles,
+    // then [s1 | s2 | perm | iters | status] ints
+    const size_t hbytes = (nin + nout) * sizeof(double) + 5 * (size_t)B * sizeof(int32_t);
+    if (t->hstage_bytes < hbytes) {
+        if (t->hstage) (void)hipHostFree(t->hstage);
+        t->hstage = nullptr;
+        t->hstage_bytes = 0;
+        hipError_t e = hipHostMalloc(&t->hstage, hbytes, hipHostMallocDefault);
+        if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_prox_batch_host pinned staging: ") + hipGetErrorString(e));
+        t->hstage_bytes = hbytes;
+    }
+    double* soa = static_cast<double*>(t->hstage);
+    double* outd = soa + nin;
+    int32_t* ids = reinterpret_cast<int32_t*>(outd + nout);
     for (int64_t i = 0; i < B; ++i)
         for (int q = 0; q < 6; ++q) {
             soa[q * B + i] = pose1[6 * i + q];
             soa[(6 + q) * B + i] = pose2[6 * i + q];
         }
-    std::vector<int32_t> ids((size_t)3 * B);
-    std::memcpy(ids.data(), s1, sizeof(int32_t) * B);
-    std::memcpy(ids.data() + B, s2, sizeof(int32_t) * B);
-    std::memcpy(ids.data() + 2 * B, perm.data(), sizeof(int32_t) * B);
-    hipError_t e = hipMemcpy(dp1, soa.data(), sizeof(double) * nin, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(ib, ids.data(), sizeof(int32_t) * 3 * B, hipMemcpyHostToDevice);
+    std::memcpy(ids, s1, sizeof(int32_t) * B);
+    std::memcpy(ids + B, s2, sizeof(int32_t) * B);
+    std::memcpy(ids + 2 * B, perm.data(), sizeof(int32_t) * B);
+    // one H2D copy: [pose1 soa | pose2 soa] then [s1 | s2 | perm]
+    hipError_t e = hipMemcpy(dp1, soa, sizeof(double) * nin, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(ib, ids, sizeof(int32_t) * 3 * B, hipMemcpyHostToDevice);
     if (e == hipSuccess && segb) e = hipMemcpy(dsg, p.segs.data(), segb, hipMemcpyHostToDevice);
     if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_prox_batch_host H2D: ") + hipGetErrorString(e));
     rc = dcol_plan_run(&p, dp1, dp2, tol, max_iter, flags, dal, dct, dgr, dit, dst, nullptr);
     if (rc != DCOL_SUCCESS) return rc;
-    std::vector<double> outd(nout);
-    e = hipMemcpy(outd.data(), dal, sizeof(double) * nout, hipMemcpyDeviceToHost);   // synchronises
-    if (e == hipSuccess && iters) e = hipMemcpy(iters, dit, sizeof(int32_t) * B, hipMemcpyDeviceToHost);
-    if (e == hipSuccess && status) e = hipMemcpy(status, dst, sizeof(int32_t) * B, hipMemcpyDeviceToHost);
+    e = hipMemcpy(outd, dal, sizeof(double) * nout, hipMemcpyDeviceToHost);   // synchronises
+    if (e == hipSuccess) e = hipMemcpy(ids + 3 * B, dit, sizeof(int32_t) * 2 * B, hipMemcpyDeviceToHost);
     if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_prox_batch_host D2H: ") + hipGetErrorString(e));
-    std::memcpy(alpha, outd.data(), sizeof(double) * B);
+    if (iters) std::memcpy(iters, ids + 3 * B, sizeof(int32_t) * B);
+    if (status) std::memcpy(status, ids + 4 * B, sizeof(int32_t) * B);
+    std::memcpy(alpha, outd, sizeof(double) * B);
     if (contact && (flags & DCOL_CONTACT))
         for (int64_t i = 0; i < B; ++i)
             for (int q = 0; q < 3; ++q) contact[3 * i + q] = outd[(size_t)B + q * B + i];
