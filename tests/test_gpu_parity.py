@@ -100,3 +100,43 @@ def test_fused_launch_matches_per_bucket_launches(engine, name):
         np.testing.assert_array_equal(a[k].cpu().numpy(), b[k].cpu().numpy(), err_msg=k)
     ok = d["status"] == 0
     assert np.all(alpha_close(a["alpha"].cpu().numpy()[ok], d["alpha"][ok]))
+
+
+def test_large_shape_table_sparse_bucketing():
+    """A table of more than 2,048 shapes takes the hashed (shape1, shape2) class cache of
+    dcol_capi.cpp: bucket_pairs instead of the dense S x S one; the plan (buckets, slot
+    order, variants) and therefore the results must be bitwise those of a small table."""
+    from dcol_amd import Engine, ShapeSpec, spec_from_arrays
+    d = load_golden([p for p in golden_files() if p.endswith("synthetic_mixed.npz")][0])
+    small = Engine()
+    a1, a2 = register(small, d)
+    big = Engine()
+    for k in range(2100):                                   # distinct filler spheres first
+        big.register(ShapeSpec(1, R=0.5 + 1e-4 * k))
+    ids = np.array([big.register(spec_from_arrays(d, k)) for k in range(len(d["type"]))], dtype=np.int32)
+    b1, b2 = ids[d["s1"]], ids[d["s2"]]
+    assert len(big._specs) > 2048 and ids.min() >= 2100
+    ra = small.solve_host(a1, a2, d["pose1"], d["pose2"], grad="fd")
+    rb = big.solve_host(b1, b2, d["pose1"], d["pose2"], grad="fd")
+    for k in ("status", "iters", "alpha", "grad", "contact"):
+        np.testing.assert_array_equal(getattr(ra, k), getattr(rb, k), err_msg=k)
+    ok = d["status"] == 0
+    np.testing.assert_array_equal(rb.status, d["status"])
+    assert np.all(alpha_close(rb.alpha[ok], d["alpha"][ok]))
+
+
+def test_host_staging_regrow(engine):
+    """dcol_prox_batch_host's pinned staging grows on demand and is reused for smaller
+    batches: small -> large -> small again gives the same results as the first call."""
+    d = load_golden([p for p in golden_files() if p.endswith("synthetic_polypoly.npz")][0])
+    s1, s2 = register(engine, d)
+    n = 64
+    first = engine.solve_host(s1[:n], s2[:n], d["pose1"][:n], d["pose2"][:n], grad="fd")
+    full = engine.solve_host(s1, s2, d["pose1"], d["pose2"], grad="fd")
+    again = engine.solve_host(s1[:n], s2[:n], d["pose1"][:n], d["pose2"][:n], grad="fd")
+    for k in ("status", "iters", "alpha", "grad", "contact"):
+        np.testing.assert_array_equal(getattr(first, k), getattr(again, k), err_msg=k)
+    ok = d["status"] == 0
+    np.testing.assert_array_equal(full.status, d["status"])
+    assert np.all(alpha_close(full.alpha[ok], d["alpha"][ok]))
+    assert np.all(grad_close(full.grad[ok], d["grad"][ok]))
