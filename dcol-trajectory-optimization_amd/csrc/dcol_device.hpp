@@ -405,10 +405,12 @@ __device__ __forceinline__ double dpp_d(double v) {
 #define DCOL_XOR1(v) dpp_d<0xB1>(v)   // quad_perm [1,0,3,2]
 #define DCOL_XOR2(v) dpp_d<0x4E>(v)   // quad_perm [2,3,0,1]
 #define DCOL_HMIR(v) dpp_d<0x141>(v)  // row_half_mirror: lane i <-> 7-i within 8 lanes
+#define DCOL_RMIR(v) dpp_d<0x140>(v)  // row_mirror: lane i <-> 15-i within 16 lanes
 #else
 #define DCOL_XOR1(v) (__builtin_trap(), (v))   // multi-lane groups run on the GPU only
 #define DCOL_XOR2(v) (__builtin_trap(), (v))
 #define DCOL_HMIR(v) (__builtin_trap(), (v))
+#define DCOL_RMIR(v) (__builtin_trap(), (v))
 #endif
 
 template <int LPP>
@@ -443,6 +445,29 @@ struct Grp<8> {
         v = fmax(v, DCOL_XOR1(v));
         v = fmax(v, DCOL_XOR2(v));
         return fmax(v, DCOL_HMIR(v));
+    }
+};
+template <>
+struct Grp<16> {
+    // 8-lane sums as Grp<8>, then the row mirror pairs each lane with one of the other half
+    // (the 48-128-row buckets: polytopes / polygons with many faces)
+    DCOL_HD static double sum(double v) {
+        v = v + DCOL_XOR1(v);
+        v = v + DCOL_XOR2(v);
+        v = v + DCOL_HMIR(v);
+        return v + DCOL_RMIR(v);
+    }
+    DCOL_HD static double min(double v) {
+        v = fmin(v, DCOL_XOR1(v));
+        v = fmin(v, DCOL_XOR2(v));
+        v = fmin(v, DCOL_HMIR(v));
+        return fmin(v, DCOL_RMIR(v));
+    }
+    DCOL_HD static double max(double v) {
+        v = fmax(v, DCOL_XOR1(v));
+        v = fmax(v, DCOL_XOR2(v));
+        v = fmax(v, DCOL_HMIR(v));
+        return fmax(v, DCOL_RMIR(v));
     }
 };
 template <>

@@ -42,13 +42,13 @@ Generates dcol_variants.inc (FL = variant flags: bit 0 FULL, bit 1 BALL):
 import os
 
 OMAX = {
-    (4, 0): [4, 8, 12, 16, 24, 32],     # polytope x polytope
-    (4, 1): [2, 4, 6, 8, 12, 16, 24, 32],  # polytope x {sphere, cone}
+    (4, 0): [4, 8, 12, 16, 24, 32, 48, 64, 128],     # polytope x polytope
+    (4, 1): [2, 4, 6, 8, 12, 16, 24, 32, 48, 64, 128],  # polytope x {sphere, cone}
     (4, 2): [2],                        # {sphere, cone} x {sphere, cone}
-    (5, 1): [8, 10, 12, 16, 24, 32],    # {capsule, cylinder} x polytope
+    (5, 1): [8, 10, 12, 16, 24, 32, 48, 64, 128],    # {capsule, cylinder} x polytope
     (5, 2): [2, 4, 6, 8],               # {capsule, cylinder} x {sphere, cone}
-    (6, 1): [8, 12, 16, 24, 32],        # polygon x polytope
-    (6, 2): [2, 4, 6, 8, 12, 16, 24, 32],  # polygon x {sphere, cone}; case-4 {capsule, cylinder}^2
+    (6, 1): [8, 12, 16, 24, 32, 48, 64, 128],        # polygon x polytope
+    (6, 2): [2, 4, 6, 8, 12, 16, 24, 32, 48, 64, 128],  # polygon x {sphere, cone}; case-4 {capsule, cylinder}^2
     (7, 2): [4, 8, 12, 16, 24, 32],     # case-4 extension: {capsule, cylinder} x polygon
     (8, 2): [4, 8, 12, 16, 24, 32],     # case-4 extension: polygon x polygon
 }
@@ -96,11 +96,18 @@ def ball(n, nsoc):
 # the dense rows at LPP 2: 2.9e8).
 BALL_SKIP = {(6, 1, 12, 2)}
 BIG = 24   # OMAX >= BIG with SOC blocks: 8 lanes per pair
+# Row buckets above 32 (48, 64, 128: polytopes / polygons with many faces, up to 128
+# orthant rows per pair = two 64-face primitives) run 8 or 16 lanes per pair at one wave per
+# SIMD (16 where 8 would spill to scratch) and stay out of the fused kernel (its register
+# allocation is the maximum over its cases; plans containing them launch per bucket).
+FUSE_OMAX = 32
 
 
 def configs(n, nsoc, omax):
     if (n, nsoc, omax) in CONFIG:
         return CONFIG[(n, nsoc, omax)]
+    if omax >= 128 or (omax >= 64 and (n > 4 or nsoc > 0)):
+        return [(16, 1)]
     if omax >= BIG:
         return [(8, 1)]
     return [(4, 1)] if omax % 4 == 0 else [(2, 1)]
@@ -112,6 +119,8 @@ def fused():
         if n > 6:
             continue
         for o in os_:
+            if o > FUSE_OMAX:
+                continue
             lpp = max(l for l, _ in configs(n, s, o))
             out.append((n, s, o, lpp, 0))
             if (n, s) in FULL:

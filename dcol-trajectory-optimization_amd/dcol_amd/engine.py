@@ -58,7 +58,7 @@ def raise_for_status(status: int):
     if status == _lib.NONFINITE:
         raise ValueError("array must not contain infs or NaNs")                  # scipy check_finite
     if status == _lib.TOO_LARGE:
-        raise ValueError("pair exceeds the engine's orthant-row capacity (32 rows)")
+        raise ValueError("pair exceeds the engine's orthant-row capacity (128 rows, 64 per primitive)")
     raise RuntimeError(f"unknown dcol status {status}")
 
 

@@ -54,7 +54,7 @@ enum dcol_status {
     DCOL_UNSUPPORTED = 2, /* both primitives have extra columns (combine case 4)          */
     DCOL_NOT_PD = 3,      /* Cholesky of G'G or of the NT normal matrix failed            */
     DCOL_NONFINITE = 4,   /* a non-finite value reached a factorisation                   */
-    DCOL_TOO_LARGE = 5    /* more orthant rows than the engine's row capacity (32)        */
+    DCOL_TOO_LARGE = 5    /* more orthant rows than the engine's row capacity (128)       */
 };
 
 /* dcol_plan_run / dcol_prox_batch_host flags. */

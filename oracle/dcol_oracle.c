@@ -18,7 +18,8 @@
 #include <stdint.h>
 #include <string.h>
 
-#define MMAX 72
+#define MMAX 136   /* 2 x FMAX orthant rows + two 4-row SOC blocks */
+#define FMAX 64    /* faces / edges per primitive */
 #define NMAX 8
 
 enum { POLYTOPE = 0, SPHERE = 1, CONE = 2, CAPSULE = 3, CYLINDER = 4, POLYGON = 5 };
@@ -33,7 +34,7 @@ typedef struct {
 
 typedef struct {           /* one primitive's conic blocks */
     int no, ns, nc;        /* orthant rows, SOC rows, columns */
-    double Go[32][NMAX], ho[32];
+    double Go[FMAX][NMAX], ho[FMAX];
     double Gs[4][NMAX], hs[4];
 } Blocks;
 
@@ -72,7 +73,7 @@ static int blocks(const Shape* sh, const double r[3], const double p[3], Blocks*
     memset(b, 0, sizeof(*b));
     switch (sh->type) {
         case POLYTOPE:
-            if (sh->nh > 32) return -1;
+            if (sh->nh > FMAX) return -1;
             b->no = sh->nh; b->ns = 0; b->nc = 4;
             for (int j = 0; j < sh->nh; ++j) {
                 const double* a = sh->A + 3 * j;
@@ -121,7 +122,7 @@ static int blocks(const Shape* sh, const double r[3], const double p[3], Blocks*
             return 0;
         }
         case POLYGON:
-            if (sh->nh > 32) return -1;
+            if (sh->nh > FMAX) return -1;
             b->no = sh->nh; b->ns = 4; b->nc = 6;
             for (int j = 0; j < sh->nh; ++j) {
                 b->Go[j][3] = -sh->b[j];

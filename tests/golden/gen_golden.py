@@ -134,7 +134,7 @@ def ref_solve(o1, o2, tol):
 def run_pairs(tab, pairs, tol=1e-6, want_grad=True, name=""):
     """pairs: list of (s1, s2, pose1(6), pose2(6)).  Drives the reference."""
     B = len(pairs)
-    MM, NN = 40, 8
+    MM, NN = 136, 8
     out = dict(alpha=np.full(B, np.nan), contact=np.full((B, 3), np.nan),
                grad=np.full((B, 12), np.nan), iters=np.full(B, -1, np.int32),
                status=np.zeros(B, np.int32), x=np.full((B, NN), np.nan),
@@ -382,6 +382,34 @@ def offsets_and_edges(rng):
     return tab, pairs
 
 
+def rand_polytope(rng, k):
+    """Bounded random polytope with k faces: the 6 box normals (boundedness) plus k - 6
+    random unit normals, offsets U(0.4, 1.3)."""
+    A = np.vstack([np.eye(3), -np.eye(3), rng.normal(size=(k - 6, 3))])
+    A /= np.linalg.norm(A, axis=1, keepdims=True)
+    return mpc.PolytopeMRP(A, rng.uniform(0.4, 1.3, k))
+
+
+def large_polytopes(rng, B=360):
+    """Many-faced primitives (orthant rows 33-64 per pair: the engine's 48- and 64-row
+    buckets) against every primitive type, both orders, plus a few pairs above 64 rows
+    (the engine's TOO_LARGE)."""
+    tab = Table()
+    big = [tab.add(rand_polytope(rng, k)) for k in (20, 26, 30, 40, 58)]
+    poly40 = mpc.create_n_sided(40, 0.6)
+    big.append(tab.add(mpc.PolygonMRP(poly40["A"], poly40["b"], 0.2)))
+    small = [tab.add(rand_shape(rng, t)) for t in range(6)] + [tab.add(rand_polytope(rng, 20))]
+    pairs = []
+    for i in range(B):
+        a = big[rng.integers(len(big))]
+        b = (small + big)[rng.integers(len(small) + len(big))]
+        if a == b:
+            b = small[0]
+        pr = (a, b) if i % 2 == 0 else (b, a)
+        pairs.append((int(pr[0]), int(pr[1]), rand_pose(rng), rand_pose(rng)))
+    return tab, pairs
+
+
 def traces(rng, n=6):
     """Per-iteration (mu, sigma, step) traces of the reference for a few pairs per class."""
     rows = []
@@ -420,6 +448,7 @@ def main():
         "synthetic_polypoly": lambda: synthetic_polypoly(np.random.default_rng(0), 2000),
         "synthetic_mixed": lambda: synthetic_mixed(np.random.default_rng(1), 1500),
         "edge_cases": lambda: offsets_and_edges(np.random.default_rng(2)),
+        "large_polytopes": lambda: large_polytopes(np.random.default_rng(5)),
     }
     for name, fn in jobs.items():
         if args.only and name != args.only:
