@@ -269,9 +269,9 @@ void latency_config(Launch& L) {
 
 // Classify + bucket (counting sort by variant key).  Fills p->launches and the slot->pair
 // permutation; returns DCOL_SUCCESS or an error.
-// O(B): each distinct (shape1, shape2) is classified once (a dense S x S cache for tables of
-// up to 2048 shapes, a hash map beyond), then a stable counting sort by group, groups in key
-// order.
+// O(B): each distinct (shape1, shape2) is classified once (a dense S x S cache when S^2 is
+// at most 4M cells and small against B, else a hash map), then a stable counting sort by
+// group, groups in key order.
 int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, dcol_plan* p,
                  std::vector<int32_t>& perm, bool case4) {
     const int32_t ns = (int32_t)t->shapes.size();
@@ -296,7 +296,10 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
         g.full = g.full && c.o == c.omax;
         return it->second;
     };
-    const bool dense = (int64_t)ns * ns <= (int64_t)1 << 22;
+    // dense cache only when it is small against the batch (its fill is O(S^2): a small
+    // batch against a big table takes the hash map)
+    const int64_t cells = (int64_t)ns * ns;
+    const bool dense = cells <= ((int64_t)1 << 22) && cells <= 16 * B + 4096;
     std::vector<int32_t> cache(dense ? (size_t)ns * ns : 0, -1);
     std::unordered_map<int64_t, int32_t> sparse;
     std::vector<int32_t> gid((size_t)B);

@@ -4,7 +4,7 @@
 // tests/test_emul_golden.py.  The product library (lib/libdcol.so) never runs this path.
 #include <vector>
 
-#include "../../dcol-trajectory-optimization_amd/csrc/dcol_host.hpp"
+#include "emul_solve.hpp"
 
 using namespace dcol;
 using namespace dcol_host;
@@ -59,25 +59,16 @@ extern "C" int dcol_emul_batch(const dcol_shape_desc* shapes, int32_t n, int64_t
         const bool full = c.o == c.omax;   // both loop specialisations, as the GPU launches pick them
         // ball-SOC specialisation as the GPU plans pick it (DCOL_NO_BALL: the dense rows)
         const bool ball = c.nsoc > 0 && sh[s1[i]].soc_kind != SOC_CONE && sh[s2[i]].soc_kind != SOC_CONE && !no_ball;
-#define DCOL_EMUL(NN, NS, OM)                                                    \
-        if (c.N == NN && c.nsoc == NS && c.omax == OM) {                         \
-            if constexpr (NN == 4 && NS == 0) {   /* variants.py FULL shapes */  \
-                if (full) {                                                      \
-                    solve_one<NN, NS, OM, 1, true>(A, i, 0);                     \
-                    continue;                                                    \
-                }                                                                \
-            }                                                                    \
-            if constexpr (NS > 0 && NN <= 6) {    /* variants.py ball() */       \
-                if (ball) {                                                      \
-                    solve_one<NN, NS, OM, 1, false, true>(A, i, 0);              \
-                    continue;                                                    \
-                }                                                                \
-            }                                                                    \
-            solve_one<NN, NS, OM, 1, false>(A, i, 0);                            \
-            continue;                                                            \
+        bool done = false;
+        switch (c.N) {
+            case 4: done = emul::solve_n<4>(c, full, ball, A, i); break;
+            case 5: done = emul::solve_n<5>(c, full, ball, A, i); break;
+            case 6: done = emul::solve_n<6>(c, full, ball, A, i); break;
+            case 7: done = emul::solve_n<7>(c, full, ball, A, i); break;
+            case 8: done = emul::solve_n<8>(c, full, ball, A, i); break;
+            default: break;
         }
-        DCOL_SHAPES(DCOL_EMUL)
-#undef DCOL_EMUL
+        if (done) continue;
         return fail(DCOL_ERR_ARG, "no variant");
     }
     for (int64_t i = 0; i < B; ++i) {

@@ -1,6 +1,6 @@
 """x86 build of the device solver (tests/emul, LPP = 1) against the reference's golden
 vectors -- checks the kernel's arithmetic without a GPU.  Skipped unless the emulator has
-been built (`make -C tests/emul`, ~2-4 min of hipcc host compilation)."""
+been built (`make -C tests/emul -j6`, ~5 min of hipcc host compilation, one object per N)."""
 import ctypes
 import os
 
