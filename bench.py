@@ -260,7 +260,9 @@ def main():
         "roofline_fp64": {"bound": "fp64-valu", "achieved": flops_pair * B / (kern_ms * 1e-3) / 1e12,
                           "peak": FP64_VECTOR_PEAK_TFS, "unit": "TFLOP/s",
                           "frac": flops_pair * B / (kern_ms * 1e-3) / 1e12 / FP64_VECTOR_PEAK_TFS,
-                          "flops_per_pair": flops_pair},
+                          "flops_per_pair": flops_pair,
+                          "flops_source": "op-counting C restatement, profiles/flop_model.json"
+                          if os.path.exists(os.path.join(REPO, "profiles", "flop_model.json")) else "hand model"},
         "pipeline": {"streams": S, "note": "steps issued round-robin on S streams with separate outputs; "
                      "value/ms_per_step are the pipelined throughput, serial_* the one-stream run",
                      "serial_value": (B * world * args.steps / elapsed_serial) if elapsed_serial else value,
@@ -542,13 +544,19 @@ def altro_section():
     return out
 
 
-def flops_per_pair(iters, grad="fd"):
-    """Algorithmic FP64 operation count per pair, poly6 x poly6 (m = 12, n = 4), from the
-    hand model of SURVEY.md §8d (each +,-,*,/,sqrt = 1, following pdip.py/NT_scaling.py):
-    assembly 530 + init 777 + iters x 1682 + exit iteration 276 + gradient, where the FD
-    gradient (13 re-assemblies + z'(Gx-h)) is 8485 and the closed-form envelope gradient
-    (w = sum z_i a_i, two DCM Jacobians, three bilinear forms per primitive) is 760."""
+def flops_per_pair(iters, grad="fd", cls="polytope-polytope (bench configs[3])"):
+    """Algorithmic FP64 operation count per pair (each +, -, *, /, sqrt = 1) at the run's
+    mean Newton iteration count.  Official counts: the op-counting build of
+    the C restatement, fitted per class into profiles/flop_model.json by
+    tests/golden/gen_flop_model.py -- poly6 x poly6: assembly 512 + PDIP 1100 + 1672 per
+    iteration + FD gradient 8444 (13 Lagrangian evaluations).  The closed-form envelope
+    gradient has no reference counterpart: its 760 ops are the hand count of
+    env_grad_prim.  Without the JSON, the hand model of SURVEY.md §8d."""
     it = float(np.mean(iters)) if len(iters) else 7.0
+    path = os.path.join(REPO, "profiles", "flop_model.json")
+    if os.path.exists(path):
+        c = json.load(open(path))["classes"][cls]
+        return c["assembly"] + c["pdip_fixed"] + it * c["pdip_per_iter"] + (c["grad_fd"] if grad == "fd" else 760)
     return 530 + 777 + it * 1682 + 276 + (8485 if grad == "fd" else 760)
 
 
