@@ -18,8 +18,8 @@
 #include <stdint.h>
 #include <string.h>
 
-#define MMAX 136   /* 2 x FMAX orthant rows + two 4-row SOC blocks */
-#define FMAX 64    /* faces / edges per primitive */
+#define MMAX 136   /* 128 orthant rows (the engine's pair capacity) + two 4-row SOC blocks */
+#define FMAX 128   /* faces / edges per primitive */
 #define NMAX 8
 
 enum { POLYTOPE = 0, SPHERE = 1, CONE = 2, CAPSULE = 3, CYLINDER = 4, POLYGON = 5 };
