@@ -454,6 +454,22 @@ def run_mixed(args, world, rank, local, dev, coll_dev, dist):
         t = torch.tensor([elapsed], device=coll_dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0])
+    # solve-only duration (HIP events on the launch stream; the plan's side-stream buckets
+    # join back into it) -> FP64 roofline with the counted per-class flop model
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+    for e0, e1 in ev:
+        e0.record(stream)
+        launch()
+        e1.record(stream)
+    torch.cuda.synchronize(dev)
+    solve_ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
+    flops_local = mixed_flops(tab, s1[mine], s2[mine], out["iters"].cpu().numpy(), out["status"].cpu().numpy(), args.grad)
+    if dist is not None:
+        t = torch.tensor([solve_ms], device=coll_dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        solve_ms_max = float(t[0])
+    else:
+        solve_ms_max = solve_ms
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -472,7 +488,15 @@ def run_mixed(args, world, rank, local, dev, coll_dev, dist):
                    "gradient": args.grad, "collective": "all_gather_into_tensor of [alpha, grad(12), status, iters]",
                    "parallelism": f"dp{world} (class-balanced shards)"},
         "solve_stats": {"ok_frac": float(np.mean(status == 0)), "iters_mean": float(full[status == 0, 14].mean())},
+        "solve_ms_rank0": solve_ms, "solve_ms_max_rank": solve_ms_max,
     }
+    if flops_local is not None:
+        tf = flops_local / (solve_ms * 1e-3) / 1e12
+        line["roofline_fp64"] = {"bound": "fp64-valu", "achieved": tf, "peak": FP64_VECTOR_PEAK_TFS,
+                                 "unit": "TFLOP/s", "frac": tf / FP64_VECTOR_PEAK_TFS,
+                                 "flops_per_pair": flops_local / max(n, 1),
+                                 "note": "rank 0's shard: counted per-class flops (profiles/flop_model.json) at each "
+                                         "pair's iteration count / the shard's solve time (HIP events)"}
     if args.check:
         from oracle import c_oracle
         k = min(args.check * 8, B)
@@ -486,6 +510,27 @@ def run_mixed(args, world, rank, local, dev, coll_dev, dist):
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def mixed_flops(tab, s1, s2, iters, status, grad="fd"):
+    """Counted FP64 flops of a mixed shard: per pair, its class's model
+    (profiles/flop_model.json) at its own Newton iteration count; None without the model."""
+    path = os.path.join(REPO, "profiles", "flop_model.json")
+    if not os.path.exists(path):
+        return None
+    classes = json.load(open(path))["classes"]
+    names = {0: "polytope", 1: "sphere", 2: "cone", 3: "capsule", 4: "cylinder", 5: "polygon"}
+    k1, k2 = tab["type"][s1], tab["type"][s2]
+    total = 0.0
+    for a in range(6):
+        for b in range(6):
+            m = (k1 == a) & (k2 == b) & (status == 0)
+            if not m.any():
+                continue
+            c = classes[f"{names[a]}-{names[b]}"]
+            g = c["grad_fd"] if grad == "fd" else 760
+            total += m.sum() * (c["assembly"] + c["pdip_fixed"] + g) + c["pdip_per_iter"] * iters[m].sum()
+    return total
 
 
 def scene_batches(device):
