@@ -665,3 +665,141 @@ int dcol_prox_batch_host(const dcol_table* tc, int64_t B, const int32_t* s1, con
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------
+// multi-GPU: one all-gather of the packed per-pair record (include/dcol.h).
+// RCCL is resolved with dlopen on first use, so libdcol.so itself has no link-time
+// dependency on it (single-GPU users never load it).
+// ------------------------------------------------------------------------------------
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+namespace {
+
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    bool ok = false;
+};
+
+const Rccl& rccl() {
+    static Rccl r = [] {
+        Rccl x;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return x;
+        x.get_unique_id = reinterpret_cast<decltype(&ncclGetUniqueId)>(dlsym(h, "ncclGetUniqueId"));
+        x.init_rank = reinterpret_cast<decltype(&ncclCommInitRank)>(dlsym(h, "ncclCommInitRank"));
+        x.destroy = reinterpret_cast<decltype(&ncclCommDestroy)>(dlsym(h, "ncclCommDestroy"));
+        x.all_gather = reinterpret_cast<decltype(&ncclAllGather)>(dlsym(h, "ncclAllGather"));
+        x.error_string = reinterpret_cast<decltype(&ncclGetErrorString)>(dlsym(h, "ncclGetErrorString"));
+        x.ok = x.get_unique_id && x.init_rank && x.destroy && x.all_gather && x.error_string;
+        return x;
+    }();
+    return r;
+}
+
+std::string rccl_error(ncclResult_t r) {
+    return rccl().error_string ? rccl().error_string(r) : std::to_string((int)r);
+}
+
+}  // namespace
+
+struct dcol_comm {
+    ncclComm_t comm = nullptr;
+    int32_t nranks = 0, rank = 0, device = 0;
+};
+
+namespace dcol {
+// rec[i] = [alpha, grad(12), status, iters] (dcol_amd/dist.py REC layout); rows >= n NaN
+__global__ void __launch_bounds__(256) pack_records(int64_t n, int64_t cap, const double* alpha, const double* grad,
+                                                    const int32_t* iters, const int32_t* status, double* rec) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cap) return;
+    double* o = rec + DCOL_REC * i;
+    const double nan = __builtin_nan("");
+    if (i >= n) {
+        for (int c = 0; c < DCOL_REC; ++c) o[c] = nan;
+        return;
+    }
+    o[0] = alpha[i];
+    for (int c = 0; c < 12; ++c) o[1 + c] = grad ? grad[c * n + i] : nan;
+    o[13] = (double)status[i];
+    o[14] = (double)iters[i];
+}
+}  // namespace dcol
+
+extern "C" {
+
+int dcol_comm_unique_id(uint8_t id[DCOL_COMM_ID_BYTES]) {
+    if (!id) return fail(DCOL_ERR_ARG, "dcol_comm_unique_id: id is NULL");
+    if (!rccl().ok) return fail(DCOL_ERR_HIP, "dcol_comm_unique_id: librccl not loadable");
+    ncclUniqueId u;
+    ncclResult_t r = rccl().get_unique_id(&u);
+    if (r != ncclSuccess) return fail(DCOL_ERR_HIP, "ncclGetUniqueId: " + rccl_error(r));
+    static_assert(sizeof(u.internal) == DCOL_COMM_ID_BYTES, "unique id size");
+    std::memcpy(id, u.internal, DCOL_COMM_ID_BYTES);
+    return DCOL_SUCCESS;
+}
+
+int dcol_comm_create(const uint8_t id[DCOL_COMM_ID_BYTES], int32_t nranks, int32_t rank, int32_t device,
+                     dcol_comm** out) {
+    if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks || device < 0)
+        return fail(DCOL_ERR_ARG, "dcol_comm_create: bad arguments");
+    *out = nullptr;
+    if (!rccl().ok) return fail(DCOL_ERR_HIP, "dcol_comm_create: librccl not loadable");
+    DeviceGuard g(device);
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, DCOL_COMM_ID_BYTES);
+    auto* c = new (std::nothrow) dcol_comm();
+    if (!c) return fail(DCOL_ERR_NOMEM, "dcol_comm_create");
+    ncclResult_t r = rccl().init_rank(&c->comm, nranks, u, rank);
+    if (r != ncclSuccess) {
+        delete c;
+        return fail(DCOL_ERR_HIP, "ncclCommInitRank: " + rccl_error(r));
+    }
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = device;
+    *out = c;
+    return DCOL_SUCCESS;
+}
+
+int dcol_comm_destroy(dcol_comm* c) {
+    if (!c) return DCOL_SUCCESS;
+    if (c->comm) (void)rccl().destroy(c->comm);
+    delete c;
+    return DCOL_SUCCESS;
+}
+
+int dcol_prox_batch_multi_gpu(const dcol_plan* p, dcol_comm* c, const double* pose1, const double* pose2, double tol,
+                              int32_t max_iter, int32_t flags, int64_t cap, double* alpha, double* grad,
+                              int32_t* iters, int32_t* status, double* rec_local, double* rec_all, void* stream) {
+    if (!p || !c || !alpha || !iters || !status || !rec_local || !rec_all)
+        return fail(DCOL_ERR_ARG, "dcol_prox_batch_multi_gpu: NULL argument");
+    if (cap < p->B) return fail(DCOL_ERR_ARG, "dcol_prox_batch_multi_gpu: cap < shard size");
+    if (p->table->device != c->device)
+        return fail(DCOL_ERR_ARG, "dcol_prox_batch_multi_gpu: plan and communicator on different devices");
+    const int32_t rflags = flags & ~DCOL_CONTACT;   // the record carries no contact point
+    int rc = dcol_plan_run(p, pose1, pose2, tol, max_iter, rflags, alpha, nullptr,
+                           (rflags & (DCOL_GRAD_FD | DCOL_GRAD_ENVELOPE)) ? grad : nullptr, iters, status, stream);
+    if (rc != DCOL_SUCCESS) return rc;
+    DeviceGuard g(c->device);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const bool want_grad = (rflags & (DCOL_GRAD_FD | DCOL_GRAD_ENVELOPE)) && grad;
+    if (cap > 0) {
+        const int64_t grid = (cap + 255) / 256;
+        hipLaunchKernelGGL(pack_records, dim3(grid), dim3(256), 0, st, p->B, cap, alpha, want_grad ? grad : nullptr,
+                           iters, status, rec_local);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("pack_records: ") + hipGetErrorString(e));
+    }
+    ncclResult_t r = rccl().all_gather(rec_local, rec_all, (size_t)cap * DCOL_REC, ncclDouble, c->comm, st);
+    if (r != ncclSuccess) return fail(DCOL_ERR_HIP, "ncclAllGather: " + rccl_error(r));
+    return DCOL_SUCCESS;
+}
+
+}  // extern "C"

@@ -55,7 +55,14 @@ SIGNATURES = {
                               c_void_p, c_void_p, c_void_p, c_void_p]),
     "dcol_prox_batch_host": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_double,
                                      c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "dcol_comm_unique_id": (c_int, [c_void_p]),
+    "dcol_comm_create": (c_int, [c_void_p, c_int32, c_int32, c_int32, POINTER(c_void_p)]),
+    "dcol_comm_destroy": (c_int, [c_void_p]),
+    "dcol_prox_batch_multi_gpu": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_double, c_int32, c_int32,
+                                          c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_void_p]),
 }
+COMM_ID_BYTES = 128
 
 _lib = None
 _load_error = None

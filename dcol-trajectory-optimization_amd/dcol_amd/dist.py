@@ -96,3 +96,76 @@ def engine_solve_fn(engine, s1, s2, pose1, pose2, tol=1e-6, grad="fd"):
         res = engine.solve_host(s1[idx], s2[idx], pose1[idx], pose2[idx], tol=tol, grad=grad, contact=False)
         return {"alpha": res.alpha, "grad": res.grad, "status": res.status, "iters": res.iters}
     return fn
+
+
+class NativeComm:
+    """The C-ABI multi-GPU path (include/dcol.h: dcol_comm_*, dcol_prox_batch_multi_gpu):
+    an RCCL communicator owned by libdcol.so, for hosts that do not run torch.distributed.
+    Rank 0 creates the id (``NativeComm.unique_id()``) and ships it to the other ranks by
+    any means; every rank then builds ``NativeComm(id, world, rank, device)``."""
+
+    def __init__(self, uid: bytes, world: int, rank: int, device: int = 0):
+        import ctypes
+        from . import _lib
+        if len(uid) != _lib.COMM_ID_BYTES:
+            raise ValueError(f"communicator id must be {_lib.COMM_ID_BYTES} bytes")
+        self.world, self.rank, self.device = int(world), int(rank), int(device)
+        buf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(uid)
+        h = ctypes.c_void_p()
+        _lib.check(_lib.load().dcol_comm_create(ctypes.cast(buf, ctypes.c_void_p), self.world, self.rank,
+                                                self.device, ctypes.byref(h)), "dcol_comm_create")
+        self.handle = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes
+        from . import _lib
+        buf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)()
+        _lib.check(_lib.load().dcol_comm_unique_id(ctypes.cast(buf, ctypes.c_void_p)), "dcol_comm_unique_id")
+        return bytes(buf)
+
+    def solve_gather(self, plan, pose1, pose2, cap: int, tol=1e-6, max_iter=50, grad="fd", out=None,
+                     stream=None):
+        """Solve this rank's shard (``plan`` over its pairs; torch float64 [6, n] poses on the
+        device) and all-gather the packed records: returns (out, rec_all) with rec_all a
+        torch float64 [world * cap, REC] tensor (rank r's shard at rows r * cap), asynchronous
+        on ``stream``.  Same record layout as :meth:`ShardedBatch.gather`."""
+        import ctypes
+
+        import torch
+
+        from . import _lib
+        from .engine import alloc_outputs, grad_flag
+        n = plan.B
+        dev = torch.device("cuda", self.device)
+        for t in (pose1, pose2):
+            if t.dtype != torch.float64 or tuple(t.shape) != (6, n) or not t.is_contiguous() or t.device != dev:
+                raise ValueError(f"poses must be contiguous float64 [6, {n}] on {dev}")
+        if cap < n:
+            raise ValueError("cap must be >= the shard size")
+        flags = grad_flag(grad)
+        if out is None:
+            out = alloc_outputs(n, dev, bool(flags), False)
+        rec_local = torch.empty((cap, REC), dtype=torch.float64, device=dev)
+        rec_all = torch.empty((self.world * cap, REC), dtype=torch.float64, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        _lib.check(_lib.load().dcol_prox_batch_multi_gpu(
+            plan.handle, self.handle, ptr(pose1), ptr(pose2), float(tol), int(max_iter), flags, int(cap),
+            ptr(out["alpha"]), ptr(out.get("grad")), ptr(out["iters"]), ptr(out["status"]), ptr(rec_local),
+            ptr(rec_all), ctypes.c_void_p(stream.cuda_stream)), "dcol_prox_batch_multi_gpu")
+        return out, rec_all
+
+    def close(self):
+        from . import _lib
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            _lib.load().dcol_comm_destroy(h)
+        self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

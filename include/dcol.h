@@ -154,6 +154,31 @@ int dcol_prox_batch_host(const dcol_table* table, int64_t B, const int32_t* shap
                          double tol, int32_t max_iter, int32_t flags, double* alpha,
                          double* contact, double* grad, int32_t* iters, int32_t* status);
 
+/* ---- multi-GPU ------------------------------------------------------
+ * One process per GPU.  Pairs are independent, so each rank solves its own shard with its
+ * own plan; when one consumer needs the whole batch, dcol_prox_batch_multi_gpu packs the
+ * shard's results and performs ONE all-gather (RCCL over xGMI, librccl loaded on first
+ * use).  Bootstrap: rank 0 calls dcol_comm_unique_id and ships the 128 bytes to the other
+ * ranks by the host's own means (the reference's Python: torch.distributed / a file).  */
+#define DCOL_COMM_ID_BYTES 128
+#define DCOL_REC 15 /* packed per-pair record: alpha, grad[12], status, iters (float64) */
+typedef struct dcol_comm dcol_comm;
+int dcol_comm_unique_id(uint8_t id[DCOL_COMM_ID_BYTES]);
+/* Collective over the nranks processes (ncclCommInitRank); `device` = this rank's GPU.   */
+int dcol_comm_create(const uint8_t id[DCOL_COMM_ID_BYTES], int32_t nranks, int32_t rank, int32_t device,
+                     dcol_comm** out);
+int dcol_comm_destroy(dcol_comm* comm);
+/* Solve this rank's shard (plan over its n pairs; pose1/pose2 SoA [6][n] and the
+ * alpha[n] / grad[12][n] (or NULL) / iters[n] / status[n] outputs are device arrays, as
+ * dcol_plan_run), pack row i of rec_local[cap][DCOL_REC] = [alpha, grad(12) (NaN without a
+ * gradient flag), status, iters] (rows n..cap-1 = NaN), then all-gather every rank's
+ * rec_local into rec_all[nranks * cap][DCOL_REC] (rank r's rows at r * cap).  Requires
+ * n <= cap, the same cap on every rank.  Asynchronous on `stream`; no allocation.       */
+int dcol_prox_batch_multi_gpu(const dcol_plan* plan, dcol_comm* comm, const double* pose1, const double* pose2,
+                              double tol, int32_t max_iter, int32_t flags, int64_t cap, double* alpha,
+                              double* grad, int32_t* iters, int32_t* status, double* rec_local,
+                              double* rec_all, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -140,3 +140,32 @@ def test_host_staging_regrow(engine):
     np.testing.assert_array_equal(full.status, d["status"])
     assert np.all(alpha_close(full.alpha[ok], d["alpha"][ok]))
     assert np.all(grad_close(full.grad[ok], d["grad"][ok]))
+
+
+def test_native_comm_multi_gpu_world1(engine):
+    """C-ABI multi-GPU path (dcol_comm_* + dcol_prox_batch_multi_gpu, RCCL via dlopen) at
+    world size 1: the gathered records equal the plan's own outputs bitwise, pad rows NaN.
+    (More ranks need more GPUs: RCCL refuses two ranks on one device.)"""
+    import torch
+    from dcol_amd.dist import REC, NativeComm, unpack
+    d = load_golden([p for p in golden_files() if p.endswith("synthetic_mixed.npz")][0])
+    s1, s2 = register(engine, d)
+    plan = engine.plan(s1, s2)
+    p1 = torch.from_numpy(np.ascontiguousarray(d["pose1"].T)).cuda()
+    p2 = torch.from_numpy(np.ascontiguousarray(d["pose2"].T)).cuda()
+    comm = NativeComm(NativeComm.unique_id(), 1, 0, 0)
+    try:
+        n = plan.B
+        out, rec = comm.solve_gather(plan, p1, p2, cap=n + 7, grad="fd")
+        ref = plan.run(p1, p2, grad="fd", contact=False)
+        torch.cuda.synchronize()
+    finally:
+        comm.close()
+    rec = rec.cpu().numpy()
+    assert rec.shape == (n + 7, REC) and np.all(np.isnan(rec[n:]))
+    u = unpack(rec[:n])
+    np.testing.assert_array_equal(u["alpha"], ref["alpha"].cpu().numpy())
+    np.testing.assert_array_equal(u["grad"], ref["grad"].cpu().numpy().T)
+    np.testing.assert_array_equal(u["status"], ref["status"].cpu().numpy())
+    np.testing.assert_array_equal(u["iters"], ref["iters"].cpu().numpy())
+    np.testing.assert_array_equal(u["status"], d["status"])
