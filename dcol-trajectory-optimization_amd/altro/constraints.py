@@ -18,6 +18,8 @@ host buffer, so a phase is one H2D copy, one (fused) launch and one D2H copy.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 from dcol_amd.engine import DEFAULT_TOL, PDIPFailure, default_engine, raise_for_status
@@ -57,6 +59,27 @@ class ObstacleField:
         self.batches = 0
         self.pairs = 0
         self._warm(pose_of(victim))
+        # Each phase (H2D of the victim poses -> solve -> D2H of the packed outputs) is one
+        # hipGraph replay: one submission instead of three per batch (launch-bound at ALTRO
+        # sizes).  DCOL_ALTRO_NO_GRAPH=1 keeps the eager three-call path (A/B runs).
+        self._graphs = {} if os.environ.get("DCOL_ALTRO_NO_GRAPH") else self._capture(tol, grad)
+
+    def _capture(self, tol, grad):
+        import torch
+        dev = self.pose1.device
+        cs = torch.cuda.Stream(dev)
+        graphs = {}
+        for g in (True, False):
+            launch = self.plan.bind(self.pose1, self.pose2, self.out, tol=tol, grad=grad if g else None, stream=cs)
+            n = 14 * self.B if g else 2 * self.B
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=cs):
+                self.pose1.copy_(self.h_pose1, non_blocking=True)
+                launch()
+                self.h_out[:n].copy_(self.d_out[:n], non_blocking=True)
+            graphs[g] = graph
+        torch.cuda.synchronize(dev)
+        return graphs
 
     @staticmethod
     def _views(flat, B):
@@ -79,10 +102,14 @@ class ObstacleField:
         P = np.asarray(victim_poses, dtype=np.float64).reshape(self.N, 6)
         hp = self.h_pose1.numpy()
         hp[:] = np.repeat(P.T, self.n_obs, axis=1)
-        self.pose1.copy_(self.h_pose1, non_blocking=True)
-        self._launch[bool(grad)]()
-        n = 14 * self.B if grad else 2 * self.B      # alpha-only phases skip the gradient block
-        self.h_out[:n].copy_(self.d_out[:n], non_blocking=True)
+        graph = self._graphs.get(bool(grad))
+        if graph is not None:
+            graph.replay()                           # on self.stream (the current stream)
+        else:
+            self.pose1.copy_(self.h_pose1, non_blocking=True)
+            self._launch[bool(grad)]()
+            n = 14 * self.B if grad else 2 * self.B  # alpha-only phases skip the gradient block
+            self.h_out[:n].copy_(self.d_out[:n], non_blocking=True)
         self.stream.synchronize()
         self.batches += 1
         self.pairs += self.B
