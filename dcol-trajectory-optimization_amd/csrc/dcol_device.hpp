@@ -294,7 +294,7 @@ DCOL_HD void soc_nt(const double* s, const double* z, SocNT& W) {
     W.w0 = (sb[0] + zb[0]) * i2g;
 #pragma unroll
     for (int k = 0; k < 3; ++k) W.w1[k] = (sb[k + 1] - zb[k + 1]) * i2g;
-    W.bf = frcp(W.w0 + 1.0);
+    W.bf = frcp1(W.w0 + 1.0);
 #if defined(__HIP_DEVICE_COMPILE__)
     // line-search scalars from the normalisation rsqrts (same J expressions as soc_ls_inv);
     // J below the reference's 1e-25 floor (or NaN) takes 1/sqrt(1e-25)
@@ -304,8 +304,8 @@ DCOL_HD void soc_nt(const double* s, const double* z, SocNT& W) {
     W.lis[0] = frsqrt(fmax(Js, 1e-25));
     W.lis[1] = frsqrt(fmax(Jz, 1e-25));
 #endif
-    W.lrc[0] = frcp(fma(s[0], W.lis[0], 1.0));
-    W.lrc[1] = frcp(fma(z[0], W.lis[1], 1.0));
+    W.lrc[0] = frcp1(fma(s[0], W.lis[0], 1.0));
+    W.lrc[1] = frcp1(fma(z[0], W.lis[1], 1.0));
 #if defined(__HIP_DEVICE_COMPILE__)
     // eta = (J(s)/J(z))^(1/4) = sqrt(u), u = sqrt(J(s)) / sqrt(J(z)) = J(s) is iz from the
     // normalisations above: one reciprocal square root instead of two sqrt sequences and two
@@ -315,8 +315,8 @@ DCOL_HD void soc_nt(const double* s, const double* z, SocNT& W) {
     W.eta = (Jz != 0.0) ? u * ie : 1.0;                     // quirk Q9
     W.ieta = (Jz != 0.0) ? ie : 1.0;
 #else
-    W.eta = (Jz != 0.0) ? sqrt(sqrt(Js * frcp(Jz))) : 1.0;   // quirk Q9
-    W.ieta = frcp(W.eta);
+    W.eta = (Jz != 0.0) ? sqrt(sqrt(Js * frcp1(Jz))) : 1.0;   // quirk Q9
+    W.ieta = frcp1(W.eta);
 #endif
 }
 
@@ -363,8 +363,8 @@ DCOL_HD void soc_prod(const double* u, const double* v, double* out) {
 DCOL_HD void soc_iprod(const double* u, const double* w, double* out) {
     const double rho = u[0] * u[0] - (u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
     const double nu = u[1] * w[1] + u[2] * w[2] + u[3] * w[3];
-    const double irho = frcp(rho);
-    const double iu0 = frcp(u[0]);
+    const double irho = frcp1(rho);
+    const double iu0 = frcp1(u[0]);
     const double c1 = nu * iu0 - w[0];
     const double c2 = rho * iu0;
     out[0] = irho * (u[0] * w[0] - nu);
@@ -1024,7 +1024,7 @@ struct Solver {
             double cmax = 1.0, p1 = 0.0, p2 = 0.0;
             predictor<FULL>(so, il, F, idg, dx, cp, dsS, dzS, cmax, p1, p2, dd);
             soc_bound(so, dsS, dzS, cmax);
-            const double aa = frcp(R::max(cmax));                   // quirk Q5 (no 0.99)
+            const double aa = frcp1(R::max(cmax));                   // quirk Q5 (no 0.99)
             DCOL_ISTAMP(it, 3);
             // rho = (s + aa ds)'(z + aa dz) / s'z, expanded as
             // s'z + aa (s'dz + z'ds) + aa^2 ds'dz (orthant sums accumulated by predictor())
@@ -1037,7 +1037,7 @@ struct Solver {
                     p1 = vs[b] ? fma(s[k], dzk, fma(z[k], dsk, p1)) : p1;
                     p2 = vs[b] ? fma(dsk, dzk, p2) : p2;
                 }
-            const double rho = (sz + R::sum(fma(aa, p1, (aa * aa) * p2))) * frcp(sz);
+            const double rho = (sz + R::sum(fma(aa, p1, (aa * aa) * p2))) * frcp1(sz);
             const double sc = fmax(0.0, fmin(1.0, rho));
             const double sigma = sc * sc * sc;                      // quirk Q6
 #pragma unroll
@@ -1071,7 +1071,7 @@ struct Solver {
                 soc_step(so[b], OR + 4 * b, sbzt[b], slds[b], dx, su[b], sdz[b], sds[b]);
                 cmax = soc_bound1(so[b].W, b, sds[b], sdz[b], cmax);
             }
-            const double a = fmin(1.0, 0.99 * frcp(R::max(cmax)));
+            const double a = fmin(1.0, 0.99 * frcp1(R::max(cmax)));
             DCOL_ISTAMP(it, 6);
 #pragma unroll
             for (int j = 0; j < N; ++j) x[j] += a * dx[j];
