@@ -12,9 +12,14 @@ buffers, as a pipelined batch service would: the last, partly-filled round of on
 waves overlaps the first round of the next.  The one-stream (serialised) throughput is
 reported beside it (pipeline.serial_value), and kernel_ms is the per-launch duration.
 
-Multi-GPU: one process per GPU (torchrun); every rank solves its own 100k-pair shard
-(independent units, no data-path collective) -> "scaling": "weak"; the timed region is
-bracketed by barrier + synchronize and the max over ranks is taken.
+Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE set) this process is one rank;
+`python bench.py --gpus N` without torchrun starts the N ranks itself (torch.distributed.run
+as a child process, before this process touches the GPU) and exits with its status.  Every
+rank solves its own 100k-pair shard (independent units, no data-path collective) ->
+"scaling": "weak"; the timed region is bracketed by barrier + synchronize and the max over
+ranks is taken.  The same line carries `mixed1m`: BASELINE configs[4] (1M mixed pairs,
+class-balanced shards over the ranks, one RCCL all-gather of the packed records) through
+the shipped C-ABI path dcol_prox_batch_multi_gpu (strong scaling).
 
 Also reported: roofline of the solve kernel (HIP-event timed on the launch stream) against
 HBM (algorithmic 208 B/pair) and against FP64 vector peak; the CPU baseline = the NumPy
@@ -108,6 +113,32 @@ def cpu_baseline_c(tab, s1, s2, p1, p2, threads, seconds=3.0):
             "per_core": done / wall / threads}
 
 
+def spawn_ranks(n):
+    """Run this script as `n` torchrun ranks (127.0.0.1 rendezvous) in a child process and
+    return its exit status.  Called before anything initialises the GPU in this process."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def cpu_share(requested=0):
+    """(workers, description) for the CPU baselines: every core this process may run on
+    (its affinity mask), bounded by the host's OMP_NUM_THREADS when set (the GPU pool pins a
+    one-GPU job's CPU share there: os.cpu_count() reports the whole machine)."""
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    share = min(avail, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else avail
+    workers = max(1, min(requested, avail) if requested > 0 else share)
+    return workers, (f"{workers} workers; {avail} CPUs in this process's affinity mask, os.cpu_count() "
+                     f"{os.cpu_count()}, OMP_NUM_THREADS {omp or 'unset'}")
+
+
 def read_traffic(profile_dir, kernel_substr="prox_kernel"):
     """Per-launch HBM bytes of the solve kernel from a committed rocprofv3 PMC pass
     (FETCH_SIZE + WRITE_SIZE in KB; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM)."""
@@ -130,7 +161,8 @@ def main():
     ap.add_argument("--pairs", type=int, default=100_000, help="pairs per GPU")
     ap.add_argument("--grad", choices=["fd", "envelope"], default="fd")
     ap.add_argument("--cpu-sample", type=int, default=16000)
-    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--cpu-workers", type=int, default=0,
+                    help="host processes / threads for the CPU baselines (0 = every core this process may run on)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check", type=int, default=256, help="pairs re-checked against the oracle")
     ap.add_argument("--max-iter", type=int, default=50, help="PDIP iteration cap (diagnostics only; reference: 50)")
@@ -144,15 +176,29 @@ def main():
                          "all-gather (strong scaling)")
     ap.add_argument("--backend", default=os.environ.get("DCOL_DIST_BACKEND", "nccl"),
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo for rehearsals)")
+    ap.add_argument("--mixed-steps", type=int, default=20,
+                    help="timed steps of the configs[4] sub-measurement (mixed1m) of the default line; 0 = skip")
+    ap.add_argument("--torch-gather", action="store_true",
+                    help="mixed1m: all-gather through torch.distributed instead of the C-ABI RCCL path")
     args = ap.parse_args()
 
-    import torch
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # N ranks requested without a launcher: start them, before this process touches the GPU
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher formed a world of {world} ranks", file=sys.stderr)
+        sys.exit(2)
+
+    import torch
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     ndev = torch.cuda.device_count()
     local = local % max(ndev, 1)    # rehearsals may run more ranks than devices (gloo)
+    if world > 1 and args.backend == "nccl" and ndev < world:
+        print(f"bench.py: {world} RCCL ranks need {world} GPUs, this node shows {ndev}", file=sys.stderr)
+        sys.exit(2)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -164,6 +210,9 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local)
     coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
+    if dist is not None and dist.get_world_size() != args.gpus:
+        print(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     if args.workload == "mixed1m":
         return run_mixed(args, world, rank, local, dev, coll_dev, dist)
 
@@ -228,6 +277,9 @@ def main():
     iters = out["iters"].cpu().numpy()
     alpha = out["alpha"].cpu().numpy()
     grad = out["grad"].cpu().numpy()
+    # configs[4] on the same ranks (every rank takes part: one all-gather per step)
+    mixed = (mixed_measure(args, world, rank, local, dev, coll_dev, dist, args.mixed_steps, min(args.warmup, 5))
+             if args.mixed_steps > 0 else None)
 
     if rank != 0:
         dist.destroy_process_group()
@@ -269,6 +321,8 @@ def main():
                      "serial_ms_per_step": 1e3 * (elapsed_serial or elapsed) / args.steps},
         "kernel_ms": kern_ms,
         "kernel_ms_max_rank": kern_ms_max,
+        "world": {"ranks": world, "process_group_size": dist.get_world_size() if dist is not None else 1,
+                  "backend": args.backend if dist is not None else None, "devices_visible": ndev},
         "solve_stats": {"ok_frac": float(np.mean(status == 0)), "iters_mean": float(iters[status == 0].mean()),
                         "iters_max": int(iters.max()),
                         "iters_hist": np.bincount(iters, minlength=int(iters.max()) + 1).tolist()},
@@ -286,13 +340,17 @@ def main():
                       <= 1e-5 * np.maximum(np.abs(ref["grad"][ok]).max(1), 1))
         line["parity_check"] = {"pairs": int(n), "status_equal": bool(np.array_equal(status[:n], ref["status"])),
                                 "alpha_ok": bool(a_ok), "grad_ok": bool(g_ok)}
+    if mixed is not None:
+        line["mixed1m"] = mixed
     if world == 1 and not args.no_altro:
         line["altro"] = altro_section()
         line["scene_batches"] = scene_batches(local)
     if world == 1 and not args.no_cpu:
-        workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
+        workers, host = cpu_share(args.cpu_workers)
         line["cpu_baseline"] = cpu_baseline(tab, s1, s2, p1, p2, args.cpu_sample, workers)
         line["cpu_baseline_c"] = cpu_baseline_c(tab, s1, s2, p1, p2, workers)
+        for k in ("cpu_baseline", "cpu_baseline_c"):
+            line[k]["host_cpus"] = host
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
@@ -399,15 +457,28 @@ def mixed_pairs(tab, B, seed):
 
 
 def run_mixed(args, world, rank, local, dev, coll_dev, dist):
+    """--workload mixed1m: BASELINE configs[4] as the bench line itself (strong scaling)."""
+    line = mixed_measure(args, world, rank, local, dev, coll_dev, dist, args.steps, args.warmup)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
     """BASELINE configs[4]: 1M mixed-primitive pairs sharded over the ranks (class-balanced
     round-robin, dcol_amd.dist.shard_indices), each shard solved on its GPU from
     HBM-resident poses, then ONE all-gather of the packed per-pair record [alpha, grad(12),
     status, iters] so every rank holds the whole batch.  The timed step = solve + pack +
-    all-gather (strong scaling: the batch is fixed as N grows)."""
+    all-gather (strong scaling: the batch is fixed as N grows).  With the RCCL backend the
+    step is the shipped C-ABI path: dcol_prox_batch_multi_gpu (plan run -> pack_records
+    kernel -> ncclAllGather on the launch stream, communicator from dcol_comm_create);
+    gloo rehearsals (several ranks on one GPU, which RCCL refuses) and --torch-gather go
+    through torch.distributed.  Returns the line (rank 0) or None."""
     import torch
     from dcol_amd import Engine, alloc_outputs, spec_from_arrays
-    from dcol_amd.dist import REC, shard_indices
-    B = args.pairs if args.pairs != 100_000 else 1_000_000
+    from dcol_amd.dist import REC, NativeComm, shard_indices
+    B = args.pairs if (args.workload == "mixed1m" and args.pairs != 100_000) else 1_000_000
     tab = mixed_table()
     s1, s2, p1, p2 = mixed_pairs(tab, B, seed=0)
     cost = tab["type"][s1] * 8 + tab["type"][s2]          # class key for balanced dealing
@@ -422,29 +493,41 @@ def run_mixed(args, world, rank, local, dev, coll_dev, dist):
     out = alloc_outputs(len(mine), dev, want_grad=True, want_contact=False)
     stream = torch.cuda.current_stream(dev)
     launch = plan.bind(d1, d2, out, grad=args.grad, contact=False, stream=stream)
-    rec = torch.full((cap, REC), float("nan"), dtype=torch.float64, device=dev)
-    gathered = torch.empty((world * cap, REC), dtype=torch.float64, device=coll_dev)
     n = len(mine)
-
-    def step():
-        launch()
-        rec[:n, 0] = out["alpha"]
-        rec[:n, 1:13] = out["grad"].T
-        rec[:n, 13] = out["status"].to(torch.float64)
-        rec[:n, 14] = out["iters"].to(torch.float64)
+    comm, path = None, "torch.distributed all_gather_into_tensor" if dist is not None else "local copy (world 1)"
+    if args.backend == "nccl" and not args.torch_gather:
+        uid = [NativeComm.unique_id() if rank == 0 else None]
         if dist is not None:
-            dist.all_gather_into_tensor(gathered, rec.to(coll_dev))
-        else:
-            gathered.copy_(rec)
+            dist.broadcast_object_list(uid, src=0)
+        comm = NativeComm(uid[0], world, rank, local)
+        path = "C-ABI dcol_prox_batch_multi_gpu (pack_records + ncclAllGather, RCCL)"
+    rec = torch.full((cap, REC), float("nan"), dtype=torch.float64, device=dev)
+    gathered = torch.empty((world * cap, REC), dtype=torch.float64, device=dev if comm is not None else coll_dev)
 
-    for _ in range(args.warmup):
+    if comm is not None:
+        def step():
+            comm.solve_gather(plan, d1, d2, cap, grad=args.grad, out=out, stream=stream, rec_local=rec,
+                              rec_all=gathered)
+    else:
+        def step():
+            launch()
+            rec[:n, 0] = out["alpha"]
+            rec[:n, 1:13] = out["grad"].T
+            rec[:n, 13] = out["status"].to(torch.float64)
+            rec[:n, 14] = out["iters"].to(torch.float64)
+            if dist is not None:
+                dist.all_gather_into_tensor(gathered, rec.to(coll_dev))
+            else:
+                gathered.copy_(rec)
+
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize(dev)
     if dist is not None:
@@ -470,26 +553,29 @@ def run_mixed(args, world, rank, local, dev, coll_dev, dist):
         solve_ms_max = float(t[0])
     else:
         solve_ms_max = solve_ms
-    if rank != 0:
-        dist.destroy_process_group()
-        return
     allrec = gathered.cpu().numpy().reshape(world, cap, REC)
+    if comm is not None:
+        comm.close()
+    if rank != 0:
+        return None
     full = np.empty((B, REC))
     for r, ix in enumerate(idx):
         full[ix] = allrec[r, :len(ix)]
     status = full[:, 13].astype(np.int32)
     line = {
-        "metric": "PDIP proximity+grad pair-solves/sec", "value": B * args.steps / elapsed, "unit": "pair-solves/s",
-        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+        "metric": "PDIP proximity+grad pair-solves/sec", "value": B * steps / elapsed, "unit": "pair-solves/s",
+        "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": 1e3 * elapsed / steps,
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": "synthetic 1M mixed-primitive pairs sharded across GPUs + RCCL all-gather "
                                "(BASELINE.json configs[4])", "pairs_total": B, "pairs_per_gpu": cap,
                    "kinds": "polytope sphere cone capsule cylinder polygon; 27 supported ordered kind pairs",
-                   "gradient": args.grad, "collective": "all_gather_into_tensor of [alpha, grad(12), status, iters]",
+                   "gradient": args.grad, "collective": f"{path}: one all-gather of [alpha, grad(12), status, iters]",
                    "parallelism": f"dp{world} (class-balanced shards)"},
         "solve_stats": {"ok_frac": float(np.mean(status == 0)), "iters_mean": float(full[status == 0, 14].mean())},
         "solve_ms_rank0": solve_ms, "solve_ms_max_rank": solve_ms_max,
     }
+    if comm is not None:
+        line["rccl_world_size"] = world
     if flops_local is not None:
         tf = flops_local / (solve_ms * 1e-3) / 1e12
         line["roofline_fp64"] = {"bound": "fp64-valu", "achieved": tf, "peak": FP64_VECTOR_PEAK_TFS,
@@ -500,16 +586,14 @@ def run_mixed(args, world, rank, local, dev, coll_dev, dist):
     if args.check:
         from oracle import c_oracle
         k = min(args.check * 8, B)
-        ref = c_oracle.run_batch(tab, s1[:k], s2[:k], p1[:k], p2[:k], want_grad=True, threads=16)
+        ref = c_oracle.run_batch(tab, s1[:k], s2[:k], p1[:k], p2[:k], want_grad=True, threads=cpu_share()[0])
         ok = ref["status"] == 0
         line["parity_check"] = {
             "pairs": int(k), "status_equal": bool(np.array_equal(status[:k], ref["status"])),
             "alpha_ok": bool(np.all(np.abs(full[:k, 0][ok] - ref["alpha"][ok]) <= 1e-6 * np.abs(ref["alpha"][ok]) + 1e-12)),
             "grad_ok": bool(np.all(np.abs(full[:k, 1:13][ok] - ref["grad"][ok]).max(1)
                                    <= 1e-5 * np.maximum(np.abs(ref["grad"][ok]).max(1), 1)))}
-    print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    return line
 
 
 def mixed_flops(tab, s1, s2, iters, status, grad="fd"):

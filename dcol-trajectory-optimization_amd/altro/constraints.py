@@ -102,14 +102,18 @@ class ObstacleField:
         P = np.asarray(victim_poses, dtype=np.float64).reshape(self.N, 6)
         hp = self.h_pose1.numpy()
         hp[:] = np.repeat(P.T, self.n_obs, axis=1)
+        import torch
         graph = self._graphs.get(bool(grad))
-        if graph is not None:
-            graph.replay()                           # on self.stream (the current stream)
-        else:
-            self.pose1.copy_(self.h_pose1, non_blocking=True)
-            self._launch[bool(grad)]()
-            n = 14 * self.B if grad else 2 * self.B  # alpha-only phases skip the gradient block
-            self.h_out[:n].copy_(self.d_out[:n], non_blocking=True)
+        # replay() and the eager copies go to the CURRENT stream: pin it to self.stream (the
+        # stream synchronised below) whatever stream context the caller is in
+        with torch.cuda.stream(self.stream):
+            if graph is not None:
+                graph.replay()
+            else:
+                self.pose1.copy_(self.h_pose1, non_blocking=True)
+                self._launch[bool(grad)]()
+                n = 14 * self.B if grad else 2 * self.B  # alpha-only phases skip the gradient block
+                self.h_out[:n].copy_(self.d_out[:n], non_blocking=True)
         self.stream.synchronize()
         self.batches += 1
         self.pairs += self.B

@@ -125,7 +125,7 @@ class NativeComm:
         return bytes(buf)
 
     def solve_gather(self, plan, pose1, pose2, cap: int, tol=1e-6, max_iter=50, grad="fd", out=None,
-                     stream=None):
+                     stream=None, rec_local=None, rec_all=None):
         """Solve this rank's shard (``plan`` over its pairs; torch float64 [6, n] poses on the
         device) and all-gather the packed records: returns (out, rec_all) with rec_all a
         torch float64 [world * cap, REC] tensor (rank r's shard at rows r * cap), asynchronous
@@ -144,12 +144,23 @@ class NativeComm:
         if cap < n:
             raise ValueError("cap must be >= the shard size")
         flags = grad_flag(grad)
-        if out is None:
-            out = alloc_outputs(n, dev, bool(flags), False)
-        rec_local = torch.empty((cap, REC), dtype=torch.float64, device=dev)
-        rec_all = torch.empty((self.world * cap, REC), dtype=torch.float64, device=dev)
         if stream is None:
             stream = torch.cuda.current_stream(dev)
+        # Buffers allocated here belong to `stream` in torch's caching allocator (allocated
+        # under it): rec_local dies when this call returns while the pack kernel and the
+        # all-gather still read it on `stream`, so its block may only be handed out again to
+        # later work on that same stream (ordered after them).  rec_local / rec_all / out may
+        # also be passed in (hot loops reuse them; then the caller owns their lifetime).
+        with torch.cuda.stream(stream):
+            if out is None:
+                out = alloc_outputs(n, dev, bool(flags), False)
+            if rec_local is None:
+                rec_local = torch.empty((cap, REC), dtype=torch.float64, device=dev)
+            if rec_all is None:
+                rec_all = torch.empty((self.world * cap, REC), dtype=torch.float64, device=dev)
+        for t, shape in ((rec_local, (cap, REC)), (rec_all, (self.world * cap, REC))):
+            if t.dtype != torch.float64 or tuple(t.shape) != shape or not t.is_contiguous() or t.device != dev:
+                raise ValueError(f"record buffers must be contiguous float64 {shape} on {dev}")
         ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
         _lib.check(_lib.load().dcol_prox_batch_multi_gpu(
             plan.handle, self.handle, ptr(pose1), ptr(pose2), float(tol), int(max_iter), flags, int(cap),

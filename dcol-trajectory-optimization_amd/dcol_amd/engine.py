@@ -213,6 +213,10 @@ class Engine:
 
     def __init__(self, device: int = 0):
         self.device = int(device)
+        # iteration cap of the object-level calls (solve_objects and the drop-in
+        # proximity_mrp / proximity_gradient): the reference's literal 50 (pdip.py:408,
+        # quirk Q4); an attribute so a caller or test can lower it for one engine
+        self.max_iter = DEFAULT_MAX_ITER
         self._specs: list[ShapeSpec] = []
         self._ids: dict[ShapeSpec, int] = {}
         self._obj_ids: dict[int, tuple[object, int]] = {}
@@ -291,10 +295,12 @@ class Engine:
                    "dcol_prox_batch_host")
         return Result(alpha, cp, g, iters, status)
 
-    def solve_objects(self, prims1, prims2, tol=DEFAULT_TOL, max_iter=DEFAULT_MAX_ITER, grad="fd",
+    def solve_objects(self, prims1, prims2, tol=DEFAULT_TOL, max_iter=None, grad="fd",
                       contact=True, case4=False) -> Result:
         """Batched form of the drop-in: two equal-length sequences of primitive objects,
-        each at its current pose."""
+        each at its current pose.  max_iter=None: the engine's cap (self.max_iter)."""
+        if max_iter is None:
+            max_iter = self.max_iter
         s1 = np.fromiter((self.register_object(o) for o in prims1), dtype=np.int32)
         s2 = np.fromiter((self.register_object(o) for o in prims2), dtype=np.int32)
         if s1.size != s2.size:

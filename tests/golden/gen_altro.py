@@ -11,9 +11,11 @@ driver on identical inputs without the reference.
 
 Plotting (utils/plots.py) is replaced by no-ops: it draws figures only and feeds nothing
 back into the optimization.  The quadrotor system imports h5py at module level
-(cluttered_hallway_quadrotor.py:2), which this image lacks, so only its initial controls
-and the decoded polytopes.jld2 arrays are stored (from gen_golden.jld2_polytopes), not a
-whole-run trace.
+(cluttered_hallway_quadrotor.py:2) and reads the four datasets of systems/polytopes.jld2
+with it (:271-279); this image has no h5py, so a minimal stand-in module is injected into
+sys.modules whose File(...)[name][:] returns the arrays decoded by this repo's own JLD2 /
+HDF5 reader (gen_golden.jld2_polytopes: the same compact datasets, same shapes as h5py
+returns them).  Nothing else of the run is touched.
 
 Usage (cwd anywhere; writes tests/golden/altro/altro_<system>.npz and
 dcol-trajectory-optimization_amd/altro/data/initial_guess.npz):
@@ -62,6 +64,26 @@ def initial_guess():
     print("initial guess:", {k: v.shape for k, v in out.items()})
 
 
+def install_h5py_standin():
+    """sys.modules['h5py'] with File(path, mode) -> {A1, b1, A2, b2} from the jld2 file
+    (decoded by gen_golden.jld2_polytopes, not by h5py; the reference only indexes [:])."""
+    import types
+    from gen_golden import jld2_polytopes
+    arrays = jld2_polytopes()
+
+    class _File(dict):
+        def __init__(self, path, mode="r"):
+            super().__init__({k: np.array(v) for k, v in arrays.items()})
+
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *exc):
+            return False
+
+    sys.modules["h5py"] = types.SimpleNamespace(File=_File)
+
+
 def run_system(name):
     import ALTRO as ref_altro
     for k in ("plot_trajectories", "plot_cost", "plot_regularization"):
@@ -70,6 +92,9 @@ def run_system(name):
         from systems.piano_mover import initialize_piano_mover as init
     elif name == "coneThroughWall":
         from systems.cone_through_wall import initialize_coneThroughWall as init
+    elif name == "quadrotor":
+        install_h5py_standin()
+        from systems.cluttered_hallway_quadrotor import initialize_quadrotor as init
     else:
         raise SystemExit(f"unsupported system {name}")
     rec = dict(reg=[], rho=[], delta_J=[], kmax=[], alpha=[], J=[])

@@ -1,7 +1,9 @@
-"""Multi-rank sharding + all-gather (dcol_amd.dist) on CPU: world_size 2, gloo backend.
+"""Multi-rank sharding + all-gather (dcol_amd.dist): world_size 2, gloo backend.
 
-Each rank solves its shard with the NumPy oracle (test infrastructure standing in for the
-per-rank GPU engine); the gathered full batch must equal a single-process solve of the
+CPU tests: each rank solves its shard with the NumPy oracle (test infrastructure standing in
+for the per-rank GPU engine).  GPU test: each rank runs the HIP engine on its shard (two
+processes on the one GPU of the box; RCCL refuses two ranks on one device, so the exchange
+is gloo).  Either way the gathered full batch must equal a single-process solve of the
 whole batch exactly (no cross-pair arithmetic exists)."""
 import os
 import socket
@@ -30,7 +32,7 @@ def _oracle_fn(d, want_grad=True):
     return fn
 
 
-def _worker(rank, world, port, path, balanced, q):
+def _worker(rank, world, port, path, balanced, q, use_engine=False):
     import sys
     import torch.distributed as dist
     from conftest import PKG, REPO
@@ -45,7 +47,14 @@ def _worker(rank, world, port, path, balanced, q):
     d = {k: (v[:B] if k in ("s1", "s2", "pose1", "pose2") else v) for k, v in d.items()}
     cost = (d["nh"][d["s1"]] + d["nh"][d["s2"]]) if balanced else None
     sb = ShardedBatch(B, rank, world, cost_key=cost)
-    local = sb.solve(_oracle_fn(d))
+    if use_engine:
+        from dcol_amd import Engine, spec_from_arrays
+        from dcol_amd.dist import engine_solve_fn
+        eng = Engine(device=0)
+        ids = np.array([eng.register(spec_from_arrays(d, k)) for k in range(len(d["type"]))], np.int32)
+        local = sb.solve(engine_solve_fn(eng, ids[d["s1"]], ids[d["s2"]], d["pose1"], d["pose2"]))
+    else:
+        local = sb.solve(_oracle_fn(d))
     full = sb.gather(local)
     if rank == 0:
         q.put({k: v for k, v in full.items()})
@@ -85,3 +94,31 @@ def test_shard_indices_partition():
                 np.testing.assert_array_equal(allidx, np.arange(B))
                 sizes = [len(p) for p in parts]
                 assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("balanced", [False, True])
+def test_gloo_world2_hip_engine_gather_equals_single(balanced):
+    """Two ranks, each solving its shard with the HIP engine (lib/libdcol.so), all-gathered
+    over gloo: bitwise equal to one process solving the whole batch with the engine."""
+    from dcol_amd import Engine, spec_from_arrays
+    path = [p for p in golden_files() if p.endswith("synthetic_mixed.npz")][0]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, path, balanced, q, True)) for r in range(2)]
+    for p in procs:
+        p.start()
+    full = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    d = load_golden(path)
+    eng = Engine(device=0)
+    ids = np.array([eng.register(spec_from_arrays(d, k)) for k in range(len(d["type"]))], np.int32)
+    ref = eng.solve_host(ids[d["s1"][:120]], ids[d["s2"][:120]], d["pose1"][:120], d["pose2"][:120], contact=False)
+    np.testing.assert_array_equal(full["status"], ref.status)
+    np.testing.assert_array_equal(full["iters"], ref.iters)
+    np.testing.assert_array_equal(full["alpha"], ref.alpha)
+    np.testing.assert_array_equal(full["grad"], ref.grad)
+    np.testing.assert_array_equal(full["status"], d["status"][:120])

@@ -1,0 +1,219 @@
+"""The drop-in Python boundary, exercised the way the reference's callers use it.
+
+The reference's system modules bind the two proximity functions by module path at import
+time (piano_mover.py:2-3, cluttered_hallway_quadrotor.py:5-6, cone_through_wall.py:4-5),
+build primitives with the constructors of primitives/misc_primitive_constructor.py, and
+overwrite ``.r`` / ``.p`` before every call (piano_mover.py:60-61, :84-85).  These tests do
+exactly that with this repository's classes and modules, against the golden vectors the
+reference produced (tests/golden/gen_golden.py):
+
+* ``proximity_mrp(prim1, prim2, pdip_tol)`` -> (np.float64 alpha, ndarray(3) contact)
+  (/root/reference/proximity/proximity.py:6, :51-54);
+* ``proximity_gradient(prim1, prim2, pdip_tol)`` -> (np.float64 alpha, ndarray(12) grad)
+  (/root/reference/proximity/proximity_gradient.py:91, :133-138);
+* the exceptions: a bare ``Exception`` after the 50-iteration cap (pdip.py:470), ``ValueError``
+  for case-4 pairs (combine_problem_matrices.py:58-70), and the unpacking ``TypeError`` of an
+  unknown object (problem_matrices.py returns None, proximity.py:23);
+* the pose / shape ownership contract of dcol_amd.Engine (poses read at every call, shape
+  fields snapshotted until ``forget``).
+
+GPU tests call the HIP library through the C-ABI (dcol_prox_batch_host); the TypeError test
+raises before any device call and runs on the CPU.
+"""
+import numpy as np
+import pytest
+
+from conftest import alpha_close, golden_files, grad_close, load_golden
+
+GOLDEN = {p.split("/")[-1][:-4]: p for p in golden_files()}
+# per-pair calls: a spread of pairs from every family (each call is one host round trip)
+PER_PAIR = 24
+
+
+def objects_from_golden(d):
+    """One primitive object per shape of a golden shape table, built with the drop-in
+    constructors (misc_primitive_constructor.py:4-88) and the table's offsets."""
+    from primitives.misc_primitive_constructor import (CapsuleMRP, ConeMRP, CylinderMRP, PolygonMRP, PolytopeMRP,
+                                                       SphereMRP)
+    objs = []
+    for k in range(len(d["type"])):
+        t, nh, off = int(d["type"][k]), int(d["nh"][k]), int(d["A_off"][k])
+        R, L, H, beta = (float(v) for v in d["params"][k])
+        A = d["A_pool"][off:off + nh]
+        b = d["b_pool"][off:off + nh]
+        o = {0: lambda: PolytopeMRP(A[:, :3].copy(), b.copy()), 1: lambda: SphereMRP(R), 2: lambda: ConeMRP(H, beta),
+             3: lambda: CapsuleMRP(R, L), 4: lambda: CylinderMRP(R, L),
+             5: lambda: PolygonMRP(A[:, :2].copy(), b.copy(), R)}[t]()
+        o.r_offset = np.array(d["r_offset"][k], dtype=np.float64)
+        o.Q_offset = np.array(d["Q_offset"][k], dtype=np.float64).reshape(3, 3)
+        objs.append(o)
+    return objs
+
+
+def pose_pair(objs, d, i):
+    """Set the two primitives of golden pair i to its poses (callers overwrite .r/.p) and
+    return them.  A pair may name the same shape twice: then two objects are needed."""
+    a, b = objs[int(d["s1"][i])], objs[int(d["s2"][i])]
+    if a is b:
+        import copy
+        b = copy.deepcopy(a)
+    a.r, a.p = list(d["pose1"][i, :3]), d["pose1"][i, 3:].copy()     # lists too (piano_mover.py:176)
+    b.r, b.p = d["pose2"][i, :3].copy(), d["pose2"][i, 3:].copy()
+    return a, b
+
+
+def spread(idx, n):
+    idx = np.asarray(idx)
+    return idx[np.linspace(0, idx.size - 1, min(n, idx.size)).astype(int)] if idx.size else idx
+
+
+def test_unknown_object_raises_typeerror():
+    """problem_matrices() returns None for an unknown class and the caller's tuple unpacking
+    raises TypeError (proximity.py:23); raised before any device work."""
+    from primitives.misc_primitive_constructor import SphereMRP
+    from proximity.proximity import proximity_mrp
+    from proximity.proximity_gradient import proximity_gradient
+
+    class Blob:
+        r = np.zeros(3)
+        p = np.zeros(3)
+
+    with pytest.raises(TypeError):
+        proximity_mrp(SphereMRP(1.0), Blob())
+    with pytest.raises(TypeError):
+        proximity_gradient(Blob(), SphereMRP(1.0))
+
+
+def test_callers_bind_by_module_path():
+    """`from proximity.proximity import proximity_mrp` (the systems' import lines) resolves to
+    this package's drop-in, and the constructors the systems import exist with the
+    reference's signatures."""
+    import inspect
+
+    from primitives import misc_primitive_constructor as mpc
+    from proximity.proximity import proximity_mrp
+    from proximity.proximity_gradient import proximity_gradient
+    assert list(inspect.signature(proximity_mrp).parameters) == ["prim1", "prim2", "pdip_tol", "verbose"]
+    assert list(inspect.signature(proximity_gradient).parameters) == ["prim1", "prim2", "pdip_tol", "verbose"]
+    assert inspect.signature(proximity_mrp).parameters["pdip_tol"].default == 1e-6
+    for name in ("SphereMRP", "PolytopeMRP", "ConeMRP", "CapsuleMRP", "CylinderMRP", "PolygonMRP",
+                 "create_rect_prism", "create_n_sided"):
+        assert callable(getattr(mpc, name))
+    assert "dcol_amd" in proximity_mrp.__module__ or proximity_mrp.__module__ == "proximity.proximity"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["scene_piano", "scene_quad", "scene_cone", "synthetic_mixed", "edge_cases",
+                                  "large_polytopes"])
+def test_per_pair_calls_match_golden(engine, name):
+    """proximity_mrp and proximity_gradient, one call per pair on primitive objects, against
+    the reference's golden alpha / contact / gradient; unsupported (case-4) pairs raise
+    ValueError from both."""
+    from proximity.proximity import proximity_mrp
+    from proximity.proximity_gradient import proximity_gradient
+    d = load_golden(GOLDEN[name])
+    objs = objects_from_golden(d)
+    tol = float(d["tol"])
+    ok = np.flatnonzero(d["status"] == 0)
+    for i in spread(ok, PER_PAIR):
+        a, b = pose_pair(objs, d, i)
+        alpha, cp = proximity_mrp(a, b, pdip_tol=tol)
+        assert isinstance(alpha, np.float64)
+        assert isinstance(cp, np.ndarray) and cp.shape == (3,) and cp.dtype == np.float64
+        assert alpha_close(alpha, d["alpha"][i]), (i, alpha, d["alpha"][i])
+        assert np.all(np.abs(cp - d["contact"][i]) <= 1e-6 * np.maximum(np.abs(d["contact"][i]), 1.0))
+        alpha2, g = proximity_gradient(a, b, pdip_tol=tol)
+        assert isinstance(alpha2, np.float64)
+        assert isinstance(g, np.ndarray) and g.shape == (12,) and g.dtype == np.float64
+        assert alpha_close(alpha2, d["alpha"][i])
+        assert grad_close(g, d["grad"][i]), (i, g, d["grad"][i])
+    for i in spread(np.flatnonzero(d["status"] == 2), 6):       # combine_problem_matrices.py:58-70
+        a, b = pose_pair(objs, d, i)
+        with pytest.raises(ValueError):
+            proximity_mrp(a, b, pdip_tol=tol)
+        with pytest.raises(ValueError):
+            proximity_gradient(a, b, pdip_tol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["scene_quad", "synthetic_mixed", "synthetic_polypoly"])
+def test_batch_forms_match_golden(engine, name):
+    """proximity_mrp_batch / proximity_gradient_batch over a whole golden set of objects."""
+    import copy
+
+    from proximity.proximity import proximity_mrp_batch
+    from proximity.proximity_gradient import proximity_gradient_batch
+    d = load_golden(GOLDEN[name])
+    objs = objects_from_golden(d)
+    p1, p2 = [], []
+    for i in range(d["s1"].size):
+        a, b = copy.copy(objs[int(d["s1"][i])]), copy.copy(objs[int(d["s2"][i])])   # shallow: shared shape data
+        a.r, a.p = d["pose1"][i, :3], d["pose1"][i, 3:]
+        b.r, b.p = d["pose2"][i, :3], d["pose2"][i, 3:]
+        p1.append(a)
+        p2.append(b)
+    tol = float(d["tol"])
+    alpha, cp, st = proximity_mrp_batch(p1, p2, pdip_tol=tol)
+    np.testing.assert_array_equal(st, d["status"])
+    ok = d["status"] == 0
+    assert np.all(alpha_close(alpha[ok], d["alpha"][ok]))
+    assert np.all(np.abs(cp[ok] - d["contact"][ok]) <= 1e-6 * np.maximum(np.abs(d["contact"][ok]), 1.0))
+    assert np.all(np.isnan(alpha[~ok]))
+    for mode in ("fd", "envelope"):
+        alpha2, g, st2 = proximity_gradient_batch(p1, p2, pdip_tol=tol, grad=mode)
+        np.testing.assert_array_equal(st2, d["status"])
+        assert np.all(alpha_close(alpha2[ok], d["alpha"][ok]))
+        assert np.all(grad_close(g[ok], d["grad"][ok]))
+
+
+@pytest.mark.gpu
+def test_iteration_cap_raises_bare_exception(engine):
+    """pdip.py:470 raises a bare Exception after its iteration cap; the drop-in raises a
+    subclass of Exception (PDIPFailure).  The cap is the literal 50, reached by no golden pair,
+    so the default engine's cap is lowered for the call."""
+    from dcol_amd import PDIPFailure, default_engine
+    from proximity.proximity import proximity_mrp
+    from proximity.proximity_gradient import proximity_gradient
+    d = load_golden(GOLDEN["synthetic_polypoly"])
+    objs = objects_from_golden(d)
+    a, b = pose_pair(objs, d, 0)
+    eng = default_engine()
+    saved = eng.max_iter
+    try:
+        eng.max_iter = 2
+        with pytest.raises(Exception) as ei:
+            proximity_mrp(a, b)
+        assert isinstance(ei.value, PDIPFailure) and not isinstance(ei.value, (ValueError, TypeError))
+        with pytest.raises(PDIPFailure):
+            proximity_gradient(a, b)
+    finally:
+        eng.max_iter = saved
+    alpha, _ = proximity_mrp(a, b)
+    assert alpha_close(alpha, d["alpha"][0])
+
+
+@pytest.mark.gpu
+def test_pose_and_shape_ownership(engine):
+    """Poses are read at every call (callers overwrite .r/.p); shape fields are snapshotted
+    the first time an object is seen, so an in-place shape edit needs Engine.forget()."""
+    from dcol_amd import default_engine
+    from primitives.misc_primitive_constructor import SphereMRP, create_rect_prism
+    from proximity.proximity import proximity_mrp
+    from proximity.proximity_gradient import proximity_gradient
+    box = create_rect_prism(1.0, 1.0, 1.0)
+    ball = SphereMRP(0.5)
+    box.r, box.p = [0.0, 0.0, 0.0], [0.0, 0.0, 0.0]
+    ball.r, ball.p = np.array([3.0, 0.0, 0.0]), np.zeros(3)
+    a1, _ = proximity_mrp(ball, box)
+    # alpha scales both primitives about their centres: touching when alpha (0.5 + 0.5) = 3
+    assert abs(a1 - 3.0) < 1e-5
+    ball.r = np.array([5.0, 0.0, 0.0])
+    a2, g2 = proximity_gradient(ball, box)
+    assert abs(a2 - 5.0) < 1e-5 and a2 > a1
+    assert abs(g2[0] - 1.0) < 1e-4 and abs(g2[6] + 1.0) < 1e-4          # d alpha / d r1_x, d r2_x
+    ball.R = 1.5                                                        # in-place shape edit
+    a3, _ = proximity_mrp(ball, box)
+    assert a3 == a2                                                     # snapshot still used
+    default_engine().forget(ball)
+    a4, _ = proximity_mrp(ball, box)
+    assert abs(a4 - 2.5) < 1e-5                                         # 5 / (1.5 + 0.5)

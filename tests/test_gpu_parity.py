@@ -169,3 +169,34 @@ def test_native_comm_multi_gpu_world1(engine):
     np.testing.assert_array_equal(u["status"], ref["status"].cpu().numpy())
     np.testing.assert_array_equal(u["iters"], ref["iters"].cpu().numpy())
     np.testing.assert_array_equal(u["status"], d["status"])
+
+
+def test_native_comm_side_stream(engine):
+    """dcol_prox_batch_multi_gpu on a non-default stream with the buffers allocated by
+    NativeComm.solve_gather (they belong to that stream in torch's allocator): the records
+    stay intact while later allocations churn on the default stream."""
+    import torch
+    from dcol_amd.dist import NativeComm, unpack
+    d = load_golden([p for p in golden_files() if p.endswith("synthetic_polypoly.npz")][0])
+    s1, s2 = register(engine, d)
+    plan = engine.plan(s1, s2)
+    p1 = torch.from_numpy(np.ascontiguousarray(d["pose1"].T)).cuda()
+    p2 = torch.from_numpy(np.ascontiguousarray(d["pose2"].T)).cuda()
+    ref = plan.run(p1, p2, grad="fd", contact=False)
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    comm = NativeComm(NativeComm.unique_id(), 1, 0, 0)
+    try:
+        recs = []
+        for _ in range(3):
+            _, rec = comm.solve_gather(plan, p1, p2, cap=plan.B, grad="fd", stream=side)
+            junk = [torch.full((plan.B, 15), 7.0, dtype=torch.float64, device="cuda") for _ in range(4)]
+            recs.append(rec)
+            del junk
+        side.synchronize()
+    finally:
+        comm.close()
+    for rec in recs:
+        u = unpack(rec.cpu().numpy())
+        np.testing.assert_array_equal(u["alpha"], ref["alpha"].cpu().numpy())
+        np.testing.assert_array_equal(u["grad"], ref["grad"].cpu().numpy().T)
