@@ -18,8 +18,9 @@ HDF5 reader (gen_golden.jld2_polytopes: the same compact datasets, same shapes a
 returns them).  Nothing else of the run is touched.
 
 Usage (cwd anywhere; writes tests/golden/altro/altro_<system>.npz and
-dcol-trajectory-optimization_amd/altro/data/initial_guess.npz):
-    PYTHONDONTWRITEBYTECODE=1 python3 tests/golden/gen_altro.py [piano_mover coneThroughWall]
+dcol-trajectory-optimization_amd/altro/data/initial_guess.npz; the quadrotor run takes
+about 47 min of one core):
+    PYTHONDONTWRITEBYTECODE=1 python3 tests/golden/gen_altro.py [piano_mover coneThroughWall quadrotor]
 """
 import ast
 import os
