@@ -45,6 +45,8 @@ SIGNATURES = {
                                     POINTER(c_int64)]),
     "dcol_altro_rollout": (c_int, [POINTER(Model), c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_double,
                                    c_void_p, c_void_p]),
+    "dcol_altro_rollouts": (c_int, [POINTER(Model), c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_int32, c_void_p, c_void_p]),
     "dcol_altro_cost": (c_int, [POINTER(Problem), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_double, POINTER(c_double)]),
     "dcol_altro_stage_terms": (c_int, [POINTER(Problem), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -163,6 +165,21 @@ def rollout(model: Model, X, U, K, k, a):
     Un = np.empty_like(U)
     _check(load().dcol_altro_rollout(ctypes.byref(model), T, _ptr(X), _ptr(U), _ptr(K), _ptr(k), float(a), _ptr(Xn),
                                      _ptr(Un)), "dcol_altro_rollout")
+    return Xn, Un
+
+
+def rollouts(model: Model, X, U, K, k, a_list):
+    """Closed-loop rollouts at several step lengths (one per host thread) -> (Xn [na, T+1, nx],
+    Un [na, T, nu]); Xn[j], Un[j] equal rollout(..., a_list[j]) bitwise."""
+    X, U, K, k = _c(X), _c(U), _c(K), _c(k)
+    a = np.ascontiguousarray(a_list, dtype=np.float64).reshape(-1)
+    T = U.shape[0]
+    if X.shape != (T + 1, model.nx) or K.shape != (T, model.nu, model.nx) or k.shape != (T, model.nu):
+        raise ValueError("rollouts: inconsistent shapes")
+    Xn = np.empty((a.size,) + X.shape)
+    Un = np.empty((a.size,) + U.shape)
+    _check(load().dcol_altro_rollouts(ctypes.byref(model), T, _ptr(X), _ptr(U), _ptr(K), _ptr(k), _ptr(a), a.size,
+                                      _ptr(Xn), _ptr(Un)), "dcol_altro_rollouts")
     return Xn, Un
 
 

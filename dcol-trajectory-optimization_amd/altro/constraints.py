@@ -56,13 +56,56 @@ class ObstacleField:
         self.h_out = torch.empty(14 * B, dtype=torch.float64, **pin)
         h = self._views(self.h_out, B)
         self.h_alpha, self.h_status, self.h_grad = h["alpha"], h["status"], h["grad"]
+        # numpy views of the pinned buffers, made once (phases are latency-bound)
+        self._hp3 = self.h_pose1.numpy().reshape(6, self.N, self.n_obs)
+        self._np_alpha, self._np_status, self._np_grad = (t.numpy() for t in (self.h_alpha, self.h_status, self.h_grad))
         self.batches = 0
         self.pairs = 0
+        self._pending = None
         self._warm(pose_of(victim))
-        # Each phase (H2D of the victim poses -> solve -> D2H of the packed outputs) is one
-        # hipGraph replay: one submission instead of three per batch (launch-bound at ALTRO
-        # sizes).  DCOL_ALTRO_NO_GRAPH=1 keeps the eager three-call path (A/B runs).
-        self._graphs = {} if os.environ.get("DCOL_ALTRO_NO_GRAPH") else self._capture(tol, grad)
+        # How a phase reaches the GPU (DCOL_ALTRO_PHASE=zero_copy|graph|eager for A/B runs):
+        #  zero_copy (default where the pinned buffers are device-mapped): ONE kernel launch
+        #    that reads the victim poses from, and writes the packed outputs to, the pinned
+        #    host buffers directly (a few KB over PCIe inside the kernel, no copy commands);
+        #  graph: H2D of the poses -> solve -> D2H of the outputs as one hipGraph replay;
+        #  eager: the same three calls issued one by one.
+        mode = os.environ.get("DCOL_ALTRO_PHASE", "eager" if os.environ.get("DCOL_ALTRO_NO_GRAPH") else "zero_copy")
+        self._graphs, self._direct = {}, {}
+        if mode == "zero_copy":
+            self._direct = self._map_host(tol, grad)
+            if not self._direct:
+                mode = "graph"
+        if mode == "graph":
+            self._graphs = self._capture(tol, grad)
+        self.mode = mode
+
+    def _map_host(self, tol, grad):
+        """Launchers whose pose1 / output pointers are the device addresses of the pinned
+        host buffers ({} if the allocations are not device-mapped)."""
+        import ctypes
+
+        from dcol_amd import _lib
+        from dcol_amd.engine import grad_flag
+        p_pose = _lib.host_device_pointer(self.h_pose1.data_ptr())
+        p_out = _lib.host_device_pointer(self.h_out.data_ptr())
+        if p_pose is None or p_out is None:
+            return {}
+        B = self.B
+        fn = _lib.load().dcol_plan_run
+        launchers = {}
+        for g in (True, False):
+            args = (self.plan.handle, ctypes.c_void_p(p_pose), ctypes.c_void_p(self.pose2.data_ptr()),
+                    ctypes.c_double(tol), ctypes.c_int32(50), ctypes.c_int32(grad_flag(grad if g else None)),
+                    ctypes.c_void_p(p_out), None, ctypes.c_void_p(p_out + 16 * B) if g else None,
+                    ctypes.c_void_p(p_out + 12 * B), ctypes.c_void_p(p_out + 8 * B),
+                    ctypes.c_void_p(self.stream.cuda_stream))
+
+            def launch(args=args):
+                rc = fn(*args)
+                if rc:
+                    _lib.check(rc, "dcol_plan_run")
+            launchers[g] = launch
+        return launchers
 
     def _capture(self, tol, grad):
         import torch
@@ -96,33 +139,50 @@ class ObstacleField:
         self._launch[False]()
         self.stream.synchronize()
 
-    def evaluate(self, victim_poses, grad: bool):
-        """victim_poses [N, 6] (r, p per knot) -> (alpha [N, n_obs], J [N, n_obs, 12] | None).
-        Raises like the reference on the first failed pair (knot-major order)."""
-        P = np.asarray(victim_poses, dtype=np.float64).reshape(self.N, 6)
-        hp = self.h_pose1.numpy()
-        hp[:] = np.repeat(P.T, self.n_obs, axis=1)
+    def submit(self, victim_poses, grad: bool):
+        """Start one phase asynchronously: victim_poses [N, 6] (r, p per knot) are staged in
+        the pinned buffer and the phase (H2D -> solve -> D2H) is queued on self.stream; the
+        host is free until collect().  One phase in flight at a time."""
         import torch
+        P = np.asarray(victim_poses, dtype=np.float64).reshape(self.N, 6)
+        self._hp3[:] = P.T[:, :, None]          # pose of knot t for each of its n_obs pairs
+        direct = self._direct.get(bool(grad))
+        if direct is not None:                  # explicit stream, no copies
+            direct()
+            self._pending = bool(grad)
+            return
         graph = self._graphs.get(bool(grad))
         # replay() and the eager copies go to the CURRENT stream: pin it to self.stream (the
-        # stream synchronised below) whatever stream context the caller is in
+        # stream synchronised in collect) whatever stream context the caller is in
         with torch.cuda.stream(self.stream):
             if graph is not None:
-                graph.replay()
-            else:
                 self.pose1.copy_(self.h_pose1, non_blocking=True)
                 self._launch[bool(grad)]()
                 n = 14 * self.B if grad else 2 * self.B  # alpha-only phases skip the gradient block
                 self.h_out[:n].copy_(self.d_out[:n], non_blocking=True)
+        self._pending = bool(grad)
+
+    def collect(self):
+        """Wait for the phase started by submit() -> (alpha [N, n_obs], J [N, n_obs, 12] |
+        None).  Raises like the reference on the first failed pair (knot-major order)."""
+        grad = self._pending
+        self._pending = None
+        if grad is None:
+            raise RuntimeError("collect() without submit()")
         self.stream.synchronize()
         self.batches += 1
         self.pairs += self.B
-        st = self.h_status.numpy()
+        st = self._np_status
         if st.any():
             raise_for_status(int(st[np.flatnonzero(st)[0]]))
-        alpha = self.h_alpha.numpy().reshape(self.N, self.n_obs).copy()
-        J = self.h_grad.numpy().T.reshape(self.N, self.n_obs, 12).copy() if grad else None
+        alpha = self._np_alpha.reshape(self.N, self.n_obs).copy()
+        J = self._np_grad.T.reshape(self.N, self.n_obs, 12).copy() if grad else None
         return alpha, J
+
+    def evaluate(self, victim_poses, grad: bool):
+        """submit() + collect()."""
+        self.submit(victim_poses, grad)
+        return self.collect()
 
 
 __all__ = ["ObstacleField", "PDIPFailure"]

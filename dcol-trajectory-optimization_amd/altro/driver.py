@@ -5,15 +5,18 @@ reference optimizer (ALTRO.py:365-488); what changes is how the work is issued:
 
   reference (per knot, per obstacle, Python)      here
   ---------------------------------------------   ------------------------------------------
-  backward_pass: at every knot, N x n_obs alpha    ONE gradient batch of N x n_obs pairs on
-    solves + N x n_obs gradient solves              the GPU (ObstacleField.evaluate, grad)
-    (ALTRO.py:268-300)                              — its alpha also serves the forward pass's
-                                                    old cost (same trajectory)
-  compute_jacobian per knot (ALTRO.py:77-100)      dcol_altro_jacobians, all knots, native
+  backward_pass: at every knot, N x n_obs alpha    nothing: the accepted line-search trial
+    solves + N x n_obs gradient solves              of the previous iteration was solved as
+    (ALTRO.py:268-300) and compute_jacobian         ONE batch of N x n_obs pairs WITH
+    per knot (ALTRO.py:77-100)                      gradients on the GPU, and the dynamics
+                                                    Jacobians of its trajectory were computed
+                                                    on the host (dcol_altro_jacobians, all
+                                                    knots) while that batch ran; only the
+                                                    first iteration launches its own batch
   Riccati loop with scipy cho_factor (:304-336)    dcol_altro_backward, native
   forward_pass: old cost recomputed per line-      old cost from the cached alpha; per trial
-    search trial, rollout + N x n_obs solves        one native rollout + ONE alpha batch
-    (:183-239)
+    search trial, rollout + N x n_obs solves        one native rollout + ONE batch (alpha and
+    (:183-239)                                      gradients, overlapped with the Jacobians)
   AL dual update re-solves N x n_obs (:444-470)    reuses the accepted trial's alpha
   cost / AL terms per knot (:103-145, :259-300)    dcol_altro_cost / dcol_altro_stage_terms,
                                                    native, whole trajectory per call
@@ -34,6 +37,8 @@ from . import _native
 from . import systems as _systems
 
 log = logging.getLogger("altro")
+
+TRIALS = 4   # line-search step lengths per batch after a rejected full step
 
 
 @dataclasses.dataclass
@@ -61,17 +66,30 @@ class AltroResult:
 
 
 class _Timed:
-    """Wraps a constraint evaluator and accounts the time spent in it."""
+    """Wraps a constraint evaluator: submit() starts a batch, collect() waits for it (an
+    evaluator without submit/collect -- e.g. a CPU one -- is evaluated synchronously at
+    collect).  Accounts the host time spent blocked in the evaluator."""
 
     def __init__(self, field):
         self.field = field
+        self.async_ = hasattr(field, "submit") and hasattr(field, "collect")
         self.seconds = 0.0
         self.batches = 0
         self.pairs = 0
+        self._job = None
 
-    def __call__(self, poses, grad):
+    def submit(self, poses, grad):
         t0 = time.perf_counter()
-        out = self.field.evaluate(poses, grad)
+        if self.async_:
+            self.field.submit(poses, grad)
+        self._job = (poses, grad)
+        self.seconds += time.perf_counter() - t0
+
+    def collect(self):
+        t0 = time.perf_counter()
+        poses, grad = self._job
+        self._job = None
+        out = self.field.collect() if self.async_ else self.field.evaluate(poses, grad)
         self.seconds += time.perf_counter() - t0
         self.batches += 1
         self.pairs += poses.shape[0] * out[0].shape[1]
@@ -114,22 +132,29 @@ def _print_iter(itr, J, dJ, kmax, a, reg, rho):
     print(f"{itr+1:3d}   {J:10.3e}  {dJ:9.2e}  {kmax:9.2e}  {a:6.4f}   {reg:9.2e}   {rho:9.2e}")
 
 
-def solve(params, X, U, prox=None, engine=None, verbose=True) -> AltroResult:
+def solve(params, X, U, prox=None, engine=None, verbose=True, prox_wide=None) -> AltroResult:
     """Run the batched ALTRO on a reference-style problem.
 
     params/X/U: as returned by altro.systems.<system>.initialize() (or the reference's own
     initialize_<system>()).  prox: constraint evaluator with
     ``evaluate(victim_poses [N, 6], grad) -> (alpha [N, n_obs], J [N, n_obs, 12] | None)``;
-    default: an ObstacleField on the GPU (constraints.py).  params['reg'] / ['rho'] /
+    default: an ObstacleField on the GPU (constraints.py).  prox_wide: the same evaluator
+    over TRIALS * N knots (line-search retries, TRIALS trajectories per batch); default: an
+    ObstacleField when prox is None, else retries go through prox one at a time.
+    params['reg'] / ['rho'] /
     ['X_hist'] / ['U_hist'] are updated in place like the reference does."""
     t_setup = time.perf_counter()
     P = _Problem(params)
     N, nx, nu = P.N, P.nx, P.nu
     X = np.array(X, dtype=np.float64).reshape(N, nx)
     U = np.array(U, dtype=np.float64).reshape(N - 1, nu)
+    wide = _Timed(prox_wide) if prox_wide is not None else None
     if prox is None:
         from .constraints import ObstacleField
         prox = ObstacleField(params["P_vic"], params["P_obs"], N, engine=engine)
+        # the same pairing over TRIALS stacked trajectories: the retries of a line search
+        # after a rejected full step, TRIALS step lengths per batch
+        wide = _Timed(ObstacleField(params["P_vic"], params["P_obs"], TRIALS * N, engine=engine))
     evaluate = _Timed(prox)
     t_start = time.perf_counter()          # one-time set-up (shape table, plan, warm-up) excluded
     ncx = P.ncx
@@ -146,30 +171,69 @@ def solve(params, X, U, prox=None, engine=None, verbose=True) -> AltroResult:
     lam = np.zeros(nx)
     res = AltroResult(X=X, U=U, converged=False, iterations=0)
     hx_cur = None            # 1 - alpha at the current X, when known from the last accepted trial
+    # (alpha, d alpha, A, B) at the current (X, U): every line-search trial is solved WITH
+    # gradients and its dynamics Jacobians are computed on the host while the GPU batch runs,
+    # so the accepted trial hands the next backward pass everything it would recompute from
+    # the same (X, U) (ALTRO.py:77-100, :268-300)
+    at_x = None
     max_iters = int(params["max_iters"])
     for itr in range(max_iters):
         rho, reg = float(params["rho"]), float(params["reg"])   # mutated in place, like the reference
         res.reg.append(reg)
         res.rho.append(rho)
         # ---------------------------------------------------------------- backward pass
-        alpha, Jp = evaluate(_native.victim_poses(P.model, X), True)
+        if at_x is None:
+            evaluate.submit(_native.victim_poses(P.model, X), True)
+            A, B = _native.jacobians(P.model, X, U)                  # overlaps the GPU batch
+            alpha, Jp = evaluate.collect()
+            at_x = (alpha, Jp, A, B)
+        alpha, Jp, A, B = at_x
         hx = 1 - alpha
         Gx = _native.constraint_jacobian(P.model, X, Jp)            # [N, ncx, nx]
-        A, B = _native.jacobians(P.model, X, U)
         lx, lu, lxx, luu, VxT, VxxT = _native.stage_terms(P.prob, X, U, hx, Gx, mu, mux, lam, rho)
         K, k, dJ = _native.backward(A, B, lx, lu, lxx, luu, VxT, VxxT, reg)
         # ---------------------------------------------------------------- forward pass
         old = P.cost(X, U, hx, mu, mux, lam, rho)
         a, J, accepted = 1.0, old, False
-        for _ in range(int(params["max_linesearch_iters"])):
-            Xn, Un = _native.rollout(P.model, X, U, K, k, a)
-            an, _ = evaluate(_native.victim_poses(P.model, Xn), False)
-            hxn = 1 - an
-            new = P.cost(Xn, Un, hxn, mu, mux, lam, rho)
-            if new < old:
-                X, U, J, accepted, hx_cur = Xn, Un, new, True, hxn
-                break
-            a *= 0.5
+        n_ls = int(params["max_linesearch_iters"])
+        tried = 0
+        while tried < n_ls and not accepted:
+            if tried == 0 or wide is None:
+                # the full step (accepted in most iterations), or every trial when no wide
+                # evaluator exists: one trajectory, Jacobians overlapped with its batch
+                Xn, Un = _native.rollout(P.model, X, U, K, k, a)
+                evaluate.submit(_native.victim_poses(P.model, Xn), True)
+                An, Bn = _native.jacobians(P.model, Xn, Un)          # overlaps the GPU batch
+                an, Jn = evaluate.collect()
+                hxn = 1 - an
+                new = P.cost(Xn, Un, hxn, mu, mux, lam, rho)
+                tried += 1
+                if new < old:
+                    X, U, J, accepted, hx_cur = Xn, Un, new, True, hxn
+                    at_x = (an, Jn, An, Bn)
+                else:
+                    a *= 0.5
+                continue
+            # retries: the next TRIALS step lengths of the reference's halving sequence in
+            # one batch; the first one that lowers the cost is taken, exactly as trying them
+            # one at a time would (later ones are discarded)
+            w = min(TRIALS, n_ls - tried)
+            steps = [a * 0.5 ** j for j in range(TRIALS)]
+            Xs, Us = _native.rollouts(P.model, X, U, K, k, steps)
+            wide.submit(_native.victim_poses(P.model, Xs.reshape(-1, nx)), True)
+            ans, Jns = wide.collect()
+            ans = ans.reshape(TRIALS, N, ncx)
+            Jns = Jns.reshape(TRIALS, N, ncx, 12)
+            for j in range(w):
+                hxn = 1 - ans[j]
+                new = P.cost(Xs[j], Us[j], hxn, mu, mux, lam, rho)
+                tried += 1
+                if new < old:
+                    X, U, J, accepted, hx_cur = Xs[j], Us[j], new, True, hxn
+                    A_, B_ = _native.jacobians(P.model, X, U)
+                    at_x = (ans[j].copy(), Jns[j].copy(), A_, B_)
+                    break
+                a *= 0.5
         if not accepted:
             log.warning("Forward pass failed to reduce cost after line search, increasing reg")
             a, hx_cur = 0.0, hx
@@ -214,6 +278,10 @@ def solve(params, X, U, prox=None, engine=None, verbose=True) -> AltroResult:
     res.wall_s = time.perf_counter() - t_start
     res.setup_s = t_start - t_setup
     res.prox_s, res.prox_batches, res.prox_pairs = evaluate.seconds, evaluate.batches, evaluate.pairs
+    if wide is not None:
+        res.prox_s += wide.seconds
+        res.prox_batches += wide.batches
+        res.prox_pairs += wide.pairs
     return res
 
 

@@ -11,6 +11,7 @@
 // to rounding; 3-term dot products inside BLAS may differ in the last bit.
 #include "../../include/dcol_altro.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -394,6 +395,17 @@ int dcol_altro_rollout(const dcol_altro_model* m, int64_t T, const double* X, co
         rk4(*m, xn, un, xn + nx);
     }
     return DCOL_ALTRO_OK;
+}
+
+int dcol_altro_rollouts(const dcol_altro_model* m, int64_t T, const double* X, const double* U, const double* K,
+                        const double* k, const double* a, int32_t na, double* Xn, double* Un) {
+    if (!model_ok(m) || T < 0 || na < 0 || (na > 0 && (!a || !X || !Xn || (T > 0 && (!U || !K || !k || !Un)))))
+        return DCOL_ALTRO_ERR_ARG;
+    const int64_t sx = (T + 1) * m->nx, su = T * m->nu;
+    int rc = DCOL_ALTRO_OK;
+#pragma omp parallel for schedule(static) if (na > 1) reduction(min : rc)
+    for (int32_t j = 0; j < na; ++j) rc = std::min(rc, dcol_altro_rollout(m, T, X, U, K, k, a[j], Xn + j * sx, Un + j * su));
+    return rc;
 }
 
 }  // extern "C"

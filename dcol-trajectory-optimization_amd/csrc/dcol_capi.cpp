@@ -714,21 +714,34 @@ struct dcol_comm {
 };
 
 namespace dcol {
-// rec[i] = [alpha, grad(12), status, iters] (dcol_amd/dist.py REC layout); rows >= n NaN
-__global__ void __launch_bounds__(256) pack_records(int64_t n, int64_t cap, const double* alpha, const double* grad,
-                                                    const int32_t* iters, const int32_t* status, double* rec) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= cap) return;
-    double* o = rec + DCOL_REC * i;
+// rec[i] = [alpha, grad(12), status, iters] (dcol_amd/dist.py REC layout); rows >= n NaN.
+// A block packs kPackRows records: each thread gathers one record's fields from the SoA
+// outputs (coalesced reads) into LDS, then the block streams the contiguous
+// kPackRows * DCOL_REC doubles out with consecutive threads on consecutive addresses
+// (coalesced writes; a record-per-thread store pattern strides 120 B per lane).
+constexpr int kPackRows = 256;
+__global__ void __launch_bounds__(kPackRows) pack_records(int64_t n, int64_t cap, const double* alpha,
+                                                          const double* grad, const int32_t* iters,
+                                                          const int32_t* status, double* rec) {
+    __shared__ double tile[kPackRows * DCOL_REC];
+    const int64_t r0 = (int64_t)blockIdx.x * kPackRows;
+    const int64_t i = r0 + threadIdx.x;
     const double nan = __builtin_nan("");
-    if (i >= n) {
+    double* o = tile + DCOL_REC * threadIdx.x;
+    if (i < n) {
+        o[0] = alpha[i];
+#pragma unroll
+        for (int c = 0; c < 12; ++c) o[1 + c] = grad ? grad[c * n + i] : nan;
+        o[13] = (double)status[i];
+        o[14] = (double)iters[i];
+    } else {
+#pragma unroll
         for (int c = 0; c < DCOL_REC; ++c) o[c] = nan;
-        return;
     }
-    o[0] = alpha[i];
-    for (int c = 0; c < 12; ++c) o[1 + c] = grad ? grad[c * n + i] : nan;
-    o[13] = (double)status[i];
-    o[14] = (double)iters[i];
+    __syncthreads();
+    const int64_t rows = (cap - r0) < kPackRows ? (cap - r0) : kPackRows;
+    double* dst = rec + DCOL_REC * r0;
+    for (int64_t e = threadIdx.x; e < rows * DCOL_REC; e += kPackRows) dst[e] = tile[e];
 }
 }  // namespace dcol
 
@@ -791,8 +804,8 @@ int dcol_prox_batch_multi_gpu(const dcol_plan* p, dcol_comm* c, const double* po
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const bool want_grad = (rflags & (DCOL_GRAD_FD | DCOL_GRAD_ENVELOPE)) && grad;
     if (cap > 0) {
-        const int64_t grid = (cap + 255) / 256;
-        hipLaunchKernelGGL(pack_records, dim3(grid), dim3(256), 0, st, p->B, cap, alpha, want_grad ? grad : nullptr,
+        const int64_t grid = (cap + kPackRows - 1) / kPackRows;
+        hipLaunchKernelGGL(pack_records, dim3(grid), dim3(kPackRows), 0, st, p->B, cap, alpha, want_grad ? grad : nullptr,
                            iters, status, rec_local);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("pack_records: ") + hipGetErrorString(e));

@@ -107,3 +107,26 @@ def device_count() -> int:
     n = c_int32(0)
     check(load().dcol_device_count(ctypes.byref(n)), "dcol_device_count")
     return int(n.value)
+
+
+_hip = None
+
+
+def host_device_pointer(ptr: int):
+    """Device address of a pinned host allocation (hipHostGetDevicePointer), or None when the
+    allocation is not mapped into the device's address space (the caller then stages
+    through copies instead)."""
+    global _hip
+    if _hip is None:
+        try:
+            _hip = ctypes.CDLL("libamdhip64.so")
+            _hip.hipHostGetDevicePointer.restype = c_int
+            _hip.hipHostGetDevicePointer.argtypes = [POINTER(c_void_p), c_void_p, ctypes.c_uint]
+        except OSError:
+            _hip = False
+    if not _hip:
+        return None
+    out = c_void_p()
+    if _hip.hipHostGetDevicePointer(ctypes.byref(out), c_void_p(ptr), 0) != 0 or not out.value:
+        return None
+    return out.value

@@ -13,7 +13,7 @@
  *     delta 1e-6) called per knot at ALTRO.py:289-290           (all knots in one call)
  *   ALTRO.py backward_pass Riccati recursion :304-336          dcol_altro_backward()
  *     (Quu = luu + B'(Vxx+reg I)B, scipy cho_factor/solve)
- *   ALTRO.py forward_pass rollout :214-217                     dcol_altro_rollout()
+ *   ALTRO.py forward_pass rollout :214-217                     dcol_altro_rollout(), dcol_altro_rollouts()
  *     (U - K(Xn - X) - a k, then discrete_dynamics)
  *   ALTRO.py compute_total_cost :103-145                       dcol_altro_cost()
  *   ALTRO.py backward_pass stage / terminal terms :254-300     dcol_altro_stage_terms()
@@ -95,6 +95,12 @@ int dcol_altro_backward(int64_t T, int32_t nx, int32_t nu, const double* A, cons
  * Xn[0] = X[0], t < T.  X [T+1, nx], U [T, nu]. */
 int dcol_altro_rollout(const dcol_altro_model* m, int64_t T, const double* X, const double* U, const double* K,
                        const double* k, double a, double* Xn, double* Un);
+
+/* na rollouts of the same gains at step lengths a[0..na) (a batch of line-search trials),
+ * one per host thread: Xn [na, T+1, nx], Un [na, T, nu]; each equals dcol_altro_rollout
+ * with a[j] bitwise. */
+int dcol_altro_rollouts(const dcol_altro_model* m, int64_t T, const double* X, const double* U, const double* K,
+                        const double* k, const double* a, int32_t na, double* Xn, double* Un);
 
 /* Augmented-Lagrangian objective of a trajectory (compute_total_cost): stage costs, AL
  * terms of the control bounds and of the collision constraints hx [N, ncx] with duals

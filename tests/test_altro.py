@@ -186,6 +186,23 @@ def test_altro_run_matches_reference_cpu_evaluator(name):
     assert params["rho"] == float(g["rho_final"]) and params["reg"] == float(g["reg_final"])
 
 
+def test_altro_wide_line_search_matches_reference_cpu_evaluator():
+    """Line-search retries batched TRIALS step lengths at a time (prox_wide) take exactly the
+    reference's decisions: the quadrotor run (13 iterations with retries, down to a = 1/512)
+    against its whole-run fixture."""
+    from altro import solve, systems
+    from altro.driver import TRIALS
+    from altro_cpu import OracleField
+    g = np.load(os.path.join(GOLDEN, "altro", "altro_quadrotor.npz"))
+    params, X, U = systems.initialize("quadrotor")
+    N = params["N"]
+    r = solve(params, X, U, prox=OracleField(params["P_vic"], params["P_obs"], N),
+              prox_wide=OracleField(params["P_vic"], params["P_obs"], TRIALS * N), verbose=False)
+    check_run(r, g)
+    trials = np.log2(1 / np.array(r.alpha)) + 1
+    assert r.prox_batches == 1 + int(np.sum(1 + np.ceil((trials - 1) / TRIALS)))
+
+
 def test_reg_max_raises_like_reference():
     """update_reg (ALTRO.py:51-74): a failed line search at reg == reg_max is a ValueError."""
     from altro import solve, systems
@@ -197,7 +214,7 @@ def test_reg_max_raises_like_reference():
         def evaluate(self, poses, grad):
             a, J = super().evaluate(poses, grad)
             Worse.calls += 1
-            return (a if grad else a * 0 - 1e6), J       # every trial looks infeasible
+            return (a if Worse.calls == 1 else a * 0 - 1e6), J       # every trial looks infeasible
     params, X, U = systems.initialize("piano_mover")
     params["reg"] = params["reg_max"]
     params["max_linesearch_iters"] = 2
@@ -216,7 +233,12 @@ def test_altro_run_matches_reference_gpu(name):
     params, X, U = systems.initialize(name)
     r = solve(params, X, U, verbose=False)
     check_run(r, g)
-    assert r.prox_batches == r.iterations + int(np.sum(np.log2(1 / np.array(r.alpha)) + 1))
+    # one batch for the first backward pass, then per iteration one for the full step and one
+    # per TRIALS retries after it: every accepted trial's batch (with gradients) serves the
+    # next backward pass
+    from altro.driver import TRIALS
+    trials = np.log2(1 / np.array(r.alpha)) + 1
+    assert r.prox_batches == 1 + int(np.sum(1 + np.ceil((trials - 1) / TRIALS)))
 
 
 @pytest.mark.gpu
@@ -241,6 +263,36 @@ def test_obstacle_field_matches_oracle(name):
     assert grad_close(J.reshape(-1, 12), Jw.reshape(-1, 12)).all()
     a2, none = gpu.evaluate(poses, False)
     assert none is None and np.array_equal(a2, a)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["piano_mover", "quadrotor", "coneThroughWall"])
+def test_obstacle_field_phase_modes_bitwise_equal(name, monkeypatch):
+    """The three ways a phase reaches the GPU -- zero-copy (kernel reads / writes the pinned
+    host buffers), one hipGraph replay of H2D + solve + D2H, and the eager calls -- give the
+    same bits, submit/collect split or not."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    from altro import systems
+    from altro.constraints import ObstacleField
+    params, X, U = systems.initialize(name)
+    mod = systems.get(name)
+    rng = np.random.default_rng(4)
+    Xs = np.array(params["Xref"], dtype=np.float64) + 0.05 * rng.normal(size=(params["N"], params["nx"]))
+    poses = mod.victim_poses(params, Xs)
+    outs = {}
+    for mode in ("zero_copy", "graph", "eager"):
+        monkeypatch.setenv("DCOL_ALTRO_PHASE", mode)
+        f = ObstacleField(params["P_vic"], params["P_obs"], params["N"])
+        outs[mode] = []
+        for g in (True, False, True):
+            f.submit(poses, g)
+            outs[mode].append(f.collect())
+        assert f.mode == mode or (mode == "zero_copy" and f.mode == "graph")
+    for mode in ("graph", "eager"):
+        for (a, J), (b, K) in zip(outs["zero_copy"], outs[mode]):
+            assert np.array_equal(a, b)
+            assert (J is None and K is None) or np.array_equal(J, K)
 
 
 # ------------------------------------------------------------------ AL objective pieces

@@ -8,11 +8,14 @@ NAME=${1:?name}
 OUT=gpurun_out/$NAME
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-B="python3 bench.py --no-cpu --no-altro --check 0 --steps 200 --warmup 100 --streams 1"
+B="python3 bench.py --no-cpu --no-altro --check 0 --steps 200 --warmup 100 --streams 1 --mixed-steps 0"
+M="python3 bench.py --workload mixed1m --no-cpu --no-altro --check 0 --steps 20 --warmup 5"
 tools/gpu_session.sh \
-  "tests|600|python3 -m pytest tests -m gpu -q -x" \
+  "tests|600|python3 -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread" \
+  "smoke|120|python3 -c 'import __graft_entry__ as g; g.smoke()'" \
   "bench_default|400|python3 bench.py" \
   "trace|300|rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- $B" \
+  "trace_mixed|300|rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace_mixed -o run -- $M" \
   "pmc_fetch|300|rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/pmc_fetch -o run -- $B" \
   "pmc_write|300|rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/pmc_write -o run -- $B" \
   "pmc_f64|300|rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 -f csv -d $OUT/pmc_f64 -o run -- $B" \

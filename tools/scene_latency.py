@@ -3,6 +3,7 @@
 wall time of the whole evaluate() call (H2D poses, fan-out launches, D2H, sync), of the
 launch alone (back-to-back, same stream), and of one launch + sync.  Run it under
 `rocprofv3 --kernel-trace` to see the per-variant kernel durations and the gaps.
+DCOL_ALTRO_PHASE=zero_copy|graph|eager selects how a phase reaches the GPU (constraints.py).
 Usage: python3 tools/scene_latency.py [reps]"""
 import json
 import os
@@ -51,7 +52,7 @@ def main():
             f._launch[True]()
         t["launch_host_ms"] = 1e3 * (time.perf_counter() - t0) / reps
         torch.cuda.synchronize()
-        print(json.dumps({"scene": name, "pairs": f.B, "launches": f.plan.num_launches,
+        print(json.dumps({"scene": name, "mode": f.mode, "pairs": f.B, "launches": f.plan.num_launches,
                           **{k: round(v, 4) for k, v in t.items()}}), flush=True)
 
 
