@@ -95,7 +95,8 @@ struct Launch {
     int N, nsoc, omax, lpp;
     bool full = false;   // every pair has o == omax: the padding-free kernel (DCOL_FULL_VARIANTS) if built
     bool ball = false;   // every SOC block is a ball block: the structured kernel (DCOL_BALL_VARIANTS) if built
-    int flags() const { return (full ? LF_FULL : 0) | (ball ? LF_BALL : 0); }
+    bool cone = false;   // every SOC block is a cone block (N = 4): DCOL_CONE_VARIANTS if built
+    int flags() const { return (full ? LF_FULL : 0) | (ball ? LF_BALL : 0) | (cone ? LF_CONE : 0); }
     int32_t code;   // reject status
     int64_t slot0, n;
     int lane = 0;   // 0 = caller's stream, 1..kSideStreams = table side stream
@@ -247,6 +248,11 @@ bool ball_disabled() {
     static const bool off = std::getenv("DCOL_NO_BALL") != nullptr;
     return off;
 }
+// DCOL_NO_CONE=1: cone-SOC pairs run the dense (padded) kernels (A/B runs, tests)
+bool cone_disabled() {
+    static const bool off = std::getenv("DCOL_NO_CONE") != nullptr;
+    return off;
+}
 
 // A launch too small to fill the GPU runs the configuration with the shortest per-pair
 // latency: fewest orthant slots per lane (omax / lpp), over the pair's bucket and the larger
@@ -288,7 +294,13 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
         const DevShape& a = t->shapes[i1];
         const DevShape& b = t->shapes[i2];
         PairClass c = classify(a, b, case4);
-        const int ball = (c.nsoc > 0 && a.soc_kind != SOC_CONE && b.soc_kind != SOC_CONE && !ball_disabled()) ? 1 : 0;
+        // SOC form: 1 every block a ball (BALL kernels), 2 every block a cone and N = 4
+        // (CONE kernels), 0 dense
+        const bool none_cone = a.soc_kind != SOC_CONE && b.soc_kind != SOC_CONE;
+        const bool all_cone = a.soc_kind != SOC_BALL && b.soc_kind != SOC_BALL;
+        const int ball = c.nsoc == 0 ? 0
+                         : (none_cone && !ball_disabled()) ? 1
+                         : (all_cone && c.N == 4 && !cone_disabled()) ? 2 : 0;
         Key k = c.status == DCOL_OK ? Key{0, c.N, c.nsoc, c.omax, c.lpp, ball, 0} : Key{1, 0, 0, 0, 0, 0, c.status};
         auto it = gid_of_key.emplace(k, (int32_t)groups.size()).first;
         if (it->second == (int32_t)groups.size()) groups.push_back(Group{k});
@@ -337,6 +349,7 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
         L.code = std::get<6>(G.key);
         L.full = L.kind == 0 && G.full;
         L.ball = L.kind == 0 && std::get<5>(G.key) == 1;
+        L.cone = L.kind == 0 && std::get<5>(G.key) == 2;
         L.slot0 = at;
         L.n = G.n;
         if (L.kind == 0 && !lpp_forced() && L.n * L.lpp < 64LL * t->simds)   // cannot fill the GPU

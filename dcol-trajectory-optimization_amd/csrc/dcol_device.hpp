@@ -41,9 +41,15 @@
 
 namespace dcol {
 
-// Fast reciprocal / reciprocal square root: the hardware estimate (v_rcp_f64 / v_rsq_f64)
-// refined by two Newton steps to full double precision (~1 ulp, not correctly rounded --
-// a rounding-level change; the host build used by tests/emul keeps IEEE division).
+// Fast reciprocal / reciprocal square root: the hardware estimate (v_rcp_f64 / v_rsq_f64,
+// measured up to 2.5e8 ulp = 2^-24.5 relative) refined by Newton steps.  Measured on MI355X
+// over 4.2M inputs spanning 2^-60..2^60 (tools/rcp_ulp.hip, profiles/r02_altro/rcp_ulp.log):
+// frcp (two steps) correctly rounded on every input; frcp1 (one step) <= 11 ulp, mean 0.59,
+// 59 % correctly rounded; frsqrt <= 2 ulp, mean 0.2.  frcp1 serves the per-iteration
+// reciprocals (rows' 1/(s z), step lengths, rho, SOC NT scalars, soc_iprod): their
+// operands carry far more than 11 ulp of rounding from the sums and cancellations that
+// form them, and the iterate sequence stays equal to the reference's on every golden
+// vector (GPU tests); the host build used by tests/emul keeps IEEE division.
 DCOL_HD double frcp(double x) {
 #if defined(__HIP_DEVICE_COMPILE__)
     double y = __builtin_amdgcn_rcp(x);
@@ -55,7 +61,7 @@ DCOL_HD double frcp(double x) {
     return 1.0 / x;
 #endif
 }
-DCOL_HD double frcp1(double x) {   // v_rcp_f64 + one Newton step (~1 ulp)
+DCOL_HD double frcp1(double x) {   // v_rcp_f64 + one Newton step (<= 11 ulp measured)
 #if defined(__HIP_DEVICE_COMPILE__)
     double y = __builtin_amdgcn_rcp(x);
     const double e = __builtin_fma(-x, y, 1.0);
@@ -266,8 +272,21 @@ DCOL_HD void dcm_jacobian(const double p[3], double dQ[3][9]) {
 }
 
 // ------------------------------------------------------------------------------------
-// second-order cone helpers (4-vectors)
+// second-order cone helpers (D-vectors: D = 4 for ball blocks and the padded dense layout,
+// D = 3 for cone blocks in the CONE kernels -- the cone's own dimension, no zero padding)
 // ------------------------------------------------------------------------------------
+// v[1:] . w[1:] and v . w, written as the sums of the D = 4 originals
+template <int D>
+DCOL_HD double tail_dot(const double* v, const double* w) {
+    if constexpr (D == 4) return v[1] * w[1] + v[2] * w[2] + v[3] * w[3];
+    else return v[1] * w[1] + v[2] * w[2];
+}
+template <int D>
+DCOL_HD double full_dot(const double* v, const double* w) {
+    if constexpr (D == 4) return v[0] * w[0] + v[1] * w[1] + v[2] * w[2] + v[3] * w[3];
+    else return v[0] * w[0] + v[1] * w[1] + v[2] * w[2];
+}
+
 struct SocNT {
     double w0, w1[3], bf, eta, ieta;
     // soc_linesearch inputs that depend only on the current s (index 0) / z (index 1), shared
@@ -278,22 +297,23 @@ struct SocNT {
 
 // soc_NT_scaling, NT_scaling.py:340-405; W = eta * Wbar,
 // Wbar = [[w0, w1'], [w1, I + bf w1 w1']], bf = 1/(w0+1), eta = (J(s)/J(z))^(1/4)
+template <int D = 4>
 DCOL_HD void soc_nt(const double* s, const double* z, SocNT& W) {
-    const double Jz = z[0] * z[0] - (z[1] * z[1] + z[2] * z[2] + z[3] * z[3]);
-    const double Js = s[0] * s[0] - (s[1] * s[1] + s[2] * s[2] + s[3] * s[3]);
+    const double Jz = z[0] * z[0] - tail_dot<D>(z, z);
+    const double Js = s[0] * s[0] - tail_dot<D>(s, s);
     const double iz = frsqrt(Jz);
     const double is = frsqrt(Js);
-    double zb[4], sb[4];
+    double zb[D], sb[D];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < D; ++k) {
         zb[k] = z[k] * iz;
         sb[k] = s[k] * is;
     }
-    const double dot = zb[0] * sb[0] + zb[1] * sb[1] + zb[2] * sb[2] + zb[3] * sb[3];
+    const double dot = full_dot<D>(zb, sb);
     const double i2g = 0.5 * frsqrt((1.0 + dot) * 0.5);   // 1/(2 gamma)
     W.w0 = (sb[0] + zb[0]) * i2g;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) W.w1[k] = (sb[k + 1] - zb[k + 1]) * i2g;
+    for (int k = 0; k < 3; ++k) W.w1[k] = (k < D - 1) ? (sb[k + 1] - zb[k + 1]) * i2g : 0.0;
     W.bf = frcp1(W.w0 + 1.0);
 #if defined(__HIP_DEVICE_COMPILE__)
     // line-search scalars from the normalisation rsqrts (same J expressions as soc_ls_inv);
@@ -321,55 +341,59 @@ DCOL_HD void soc_nt(const double* s, const double* z, SocNT& W) {
 }
 
 // out = W v
+template <int D = 4>
 DCOL_HD void soc_mul(const SocNT& W, const double* v, double* out) {
-    const double d = W.w1[0] * v[1] + W.w1[1] * v[2] + W.w1[2] * v[3];
+    const double d = (D == 4) ? W.w1[0] * v[1] + W.w1[1] * v[2] + W.w1[2] * v[3] : W.w1[0] * v[1] + W.w1[1] * v[2];
     out[0] = W.eta * (W.w0 * v[0] + d);
     const double c = W.bf * d;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) out[k + 1] = W.eta * (v[0] * W.w1[k] + v[k + 1] + c * W.w1[k]);
+    for (int k = 0; k < D - 1; ++k) out[k + 1] = W.eta * (v[0] * W.w1[k] + v[k + 1] + c * W.w1[k]);
 }
 
 // out = W^-1 v = eta^-1 J Wbar J v   (closed form; replaces cho_solve, NT_scaling.py:109)
+template <int D = 4>
 DCOL_HD void soc_solve(const SocNT& W, const double* v, double* out) {
-    const double d = W.w1[0] * v[1] + W.w1[1] * v[2] + W.w1[2] * v[3];
+    const double d = (D == 4) ? W.w1[0] * v[1] + W.w1[1] * v[2] + W.w1[2] * v[3] : W.w1[0] * v[1] + W.w1[1] * v[2];
     out[0] = W.ieta * (W.w0 * v[0] - d);
     const double c = W.bf * d;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) out[k + 1] = W.ieta * (v[k + 1] - v[0] * W.w1[k] + c * W.w1[k]);
+    for (int k = 0; k < D - 1; ++k) out[k + 1] = W.ieta * (v[k + 1] - v[0] * W.w1[k] + c * W.w1[k]);
 }
 
 // out = W^-2 v = eta^-2 J Wbar^2 J v with Wbar^2 = [[2 w0^2 - 1, 2 w0 w1'], [2 w0 w1, I + 2 w1 w1']]
 // (uses w0^2 - |w1|^2 = 1 of the NT point; one pass instead of two soc_solve)
+template <int D = 4>
 DCOL_HD void soc_w2inv(const SocNT& W, const double* v, double* out) {
-    const double d = W.w1[0] * v[1] + W.w1[1] * v[2] + W.w1[2] * v[3];
+    const double d = (D == 4) ? W.w1[0] * v[1] + W.w1[1] * v[2] + W.w1[2] * v[3] : W.w1[0] * v[1] + W.w1[1] * v[2];
     const double e2 = W.ieta * W.ieta;
     const double tw = 2.0 * W.w0;
     out[0] = e2 * ((tw * W.w0 - 1.0) * v[0] - tw * d);
     const double c = 2.0 * d - tw * v[0];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) out[k + 1] = e2 * (v[k + 1] + c * W.w1[k]);
+    for (int k = 0; k < D - 1; ++k) out[k + 1] = e2 * (v[k + 1] + c * W.w1[k]);
 }
 
 // soc_cone_product(u, v), pdip.py:165-200
+template <int D = 4>
 DCOL_HD void soc_prod(const double* u, const double* v, double* out) {
-    const double s = u[0] * v[0] + u[1] * v[1] + u[2] * v[2] + u[3] * v[3];
-    out[1] = u[0] * v[1] + v[0] * u[1];
-    out[2] = u[0] * v[2] + v[0] * u[2];
-    out[3] = u[0] * v[3] + v[0] * u[3];
+    const double s = full_dot<D>(u, v);
+#pragma unroll
+    for (int k = 1; k < D; ++k) out[k] = u[0] * v[k] + v[0] * u[k];
     out[0] = s;
 }
 
 // inverse_soc_cone_product(u, w), pdip.py:88-122
+template <int D = 4>
 DCOL_HD void soc_iprod(const double* u, const double* w, double* out) {
-    const double rho = u[0] * u[0] - (u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
-    const double nu = u[1] * w[1] + u[2] * w[2] + u[3] * w[3];
+    const double rho = u[0] * u[0] - tail_dot<D>(u, u);
+    const double nu = tail_dot<D>(u, w);
     const double irho = frcp1(rho);
     const double iu0 = frcp1(u[0]);
     const double c1 = nu * iu0 - w[0];
     const double c2 = rho * iu0;
     out[0] = irho * (u[0] * w[0] - nu);
 #pragma unroll
-    for (int k = 1; k < 4; ++k) out[k] = irho * (c1 * u[k] + c2 * w[k]);
+    for (int k = 1; k < D; ++k) out[k] = irho * (c1 * u[k] + c2 * w[k]);
 }
 
 // soc_linesearch, pdip.py:25-52 (quirk Q10: nu floored at 1e-25), in inverse form: returns
@@ -377,14 +401,15 @@ DCOL_HD void soc_iprod(const double* u, const double* w, double* out) {
 // |rho_1| > rho_0, else 1), so the caller takes one reciprocal of the combined orthant /
 // SOC maximum (bound_inv) instead of one per cone.
 // isn = 1/sqrt(nu), rc = 1/(y_0 isn + 1) come precomputed from soc_nt (SocNT::lis, lrc).
+template <int D = 4>
 DCOL_HD double soc_ls_inv(const double* y, const double* d, double isn, double rc) {
-    const double zeta = y[0] * d[0] - (y[1] * d[1] + y[2] * d[2] + y[3] * d[3]);
+    const double zeta = y[0] * d[0] - tail_dot<D>(y, d);
     const double inu = isn * isn;
     const double rho0 = zeta * inu;
     const double coef = (zeta * isn + d[0]) * rc;
     double n2 = 0.0;
 #pragma unroll
-    for (int k = 1; k < 4; ++k) {
+    for (int k = 1; k < D; ++k) {
         const double r = d[k] * isn - coef * (y[k] * inu);
         n2 += r * r;
     }
@@ -518,20 +543,23 @@ struct Grp<4> {
 // held -- scaled by sv = 1 (real block) / 0 (inert slot) -- and every product with the
 // block is written out with its zeros dropped (same nonzero terms in the same order as the
 // dense rows).  Frees 4N doubles of registers per SOC slot.
-template <int N, int NSOC, int OMAX, int LPP, bool BALL = false>
+template <int N, int NSOC, int OMAX, int LPP, bool BALL = false, bool CONE = false>
 struct Solver {
     static_assert(OMAX % LPP == 0, "OMAX must be a multiple of LPP");
+    static_assert(!(BALL && CONE) && (!CONE || N == 4), "CONE: cone-only SOC blocks of N = 4 pairs");
     static constexpr int OR = OMAX / LPP;              // orthant slots per lane
     static constexpr int SS = (NSOC + LPP - 1) / LPP;  // SOC slots per lane
-    static constexpr int M = OR + 4 * SS;              // lane-local rows
+    static constexpr int SD = CONE ? 3 : 4;            // rows per SOC slot (cones unpadded in CONE)
+    static constexpr int M = OR + SD * SS;             // lane-local rows
     static constexpr int SSA = SS > 0 ? SS : 1;
-    static constexpr int MG = BALL ? OR : M;           // rows held densely in G
+    static constexpr int MG = (BALL || CONE) ? OR : M; // rows held densely in G
     static constexpr int NX = N - 4;                   // extra primal columns
     static constexpr int NXA = NX > 0 ? NX : 1;
     using R = Grp<LPP>;
 
     double G[MG][N];
     double sv[SSA], sR[SSA], sX[SSA][3][NXA];   // BALL: structured SOC rows (see above)
+    double cq[SSA][3][3], cc0[SSA];             // CONE: row e of slot b = [cq[b][e] | e == 0 ? cc0[b] : 0]
     double s[M], z[M], r[M];   // slack, dual, primal residual G x - h
     double x[N];
     int q, o1, o, deg;
@@ -611,17 +639,35 @@ struct Solver {
                 const int off = xoff(p2);
                 sv[b] = one;
                 sR[b] = vs[b] ? (p2 ? S2.R : S1.R) : 0.0;
-                r[OR + 4 * b] = 0.0;
+                r[OR + SD * b] = 0.0;
 #pragma unroll
                 for (int k = 0; k < 3; ++k) {
                     const double c0 = (nx >= 1) ? Qe[3 * k] : 0.0, c1 = (nx >= 2) ? Qe[3 * k + 1] : 0.0;
 #pragma unroll
                     for (int j = 4; j < N; ++j) sX[b][k][j - 4] = one * excol(j, off, c0, c1);
-                    r[OR + 4 * b + 1 + k] = vs[b] ? -re[k] : 0.0;
+                    r[OR + SD * b + 1 + k] = vs[b] ? -re[k] : 0.0;
                 }
+            } else if constexpr (CONE) {
+                // cone block, problem_matrices.py:138-145: rows -E Qe' (E = diag(tanb, 1, 1)),
+                // row 0 column 3 cc = -(tanb 3H/4), h = -E Qe' re; the same products as
+                // soc_rows; an inert slot holds zero rows
+                const double tb = p2 ? S2.tanb : S1.tanb;
+                cc0[b] = vs[b] ? (p2 ? S2.cone_c : S1.cone_c) : 0.0;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const double e = (k == 0) ? tb : 1.0;
+                    const double u0 = -(e * Qe[0 + k]);
+                    const double u1 = -(e * Qe[3 + k]);
+                    const double u2 = -(e * Qe[6 + k]);
+                    cq[b][k][0] = vs[b] ? u0 : 0.0;
+                    cq[b][k][1] = vs[b] ? u1 : 0.0;
+                    cq[b][k][2] = vs[b] ? u2 : 0.0;
+                    r[OR + SD * b + k] = vs[b] ? u0 * re[0] + u1 * re[1] + u2 * re[2] : 0.0;
+                }
+                (void)kind;
             } else {
                 soc_rows(kind, p2 ? S2.R : S1.R, p2 ? S2.cone_c : S1.cone_c, p2 ? S2.tanb : S1.tanb,
-                         p2 ? S2.n_extra : S1.n_extra, xoff(p2), Qe, re, &G[OR + 4 * b], &r[OR + 4 * b]);
+                         p2 ? S2.n_extra : S1.n_extra, xoff(p2), Qe, re, &G[OR + SD * b], &r[OR + SD * b]);
             }
         }
     }
@@ -677,6 +723,8 @@ struct Solver {
     DCOL_HD double rowdot(int k, const double* v) const {
         if constexpr (BALL)
             if (k >= OR) return ball_row(k, v);
+        if constexpr (CONE)
+            if (k >= OR) return cone_row(k, v);
         double acc = G[k][0] * v[0];
 #pragma unroll
         for (int j = 1; j < N; ++j) acc += G[k][j] * v[j];
@@ -693,10 +741,26 @@ struct Solver {
         for (int i = 0; i < NX; ++i) acc = fma(sX[b][e - 1][i], v[4 + i], acc);
         return acc;
     }
-    // out += G_b' v over the 4 rows of SOC slot b (dense or structured)
+    // CONE: row e of SOC slot b times v (the dense row's nonzero terms, same order)
+    DCOL_HD double cone_row(int k, const double* v) const {
+        const int b = (k - OR) / SD, e = (k - OR) % SD;
+        double acc = cq[b][e][0] * v[0];
+        acc += cq[b][e][1] * v[1];
+        acc += cq[b][e][2] * v[2];
+        if (e == 0) acc += cc0[b] * v[3];
+        return acc;
+    }
+    // out += G_b' v over the rows of SOC slot b (dense or structured)
     DCOL_HD void soc_gtv(int b, const double* v, double* out) const {
-        const int k0 = OR + 4 * b;
-        if constexpr (BALL) {
+        const int k0 = OR + SD * b;
+        if constexpr (CONE) {
+#pragma unroll
+            for (int e = 0; e < 3; ++e) {
+#pragma unroll
+                for (int j = 0; j < 3; ++j) out[j] += cq[b][e][j] * v[e];
+                if (e == 0) out[3] += cc0[b] * v[0];
+            }
+        } else if constexpr (BALL) {
 #pragma unroll
             for (int j = 0; j < 3; ++j) out[j] = fma(-sv[b], v[j + 1], out[j]);
             out[3] = fma(-sR[b], v[0], out[3]);
@@ -711,10 +775,20 @@ struct Solver {
                 for (int j = 0; j < N; ++j) out[j] += G[k0 + e][j] * v[e];
         }
     }
-    // gt = W^-1 G_b (4 x N), the SOC block of G~ (NT_scaling.py:164-202)
-    DCOL_HD void soc_gtilde(int b, const SocNT& W, double (&gt)[4][N]) const {
-        const int k0 = OR + 4 * b;
-        if constexpr (BALL) {
+    // gt = W^-1 G_b (SD x N), the SOC block of G~ (NT_scaling.py:164-202)
+    DCOL_HD void soc_gtilde(int b, const SocNT& W, double (&gt)[SD][N]) const {
+        const int k0 = OR + SD * b;
+        if constexpr (CONE) {
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                double col[3], res[3];
+#pragma unroll
+                for (int e = 0; e < 3; ++e) col[e] = (j < 3) ? cq[b][e][j] : (e == 0 ? cc0[b] : 0.0);
+                soc_solve<3>(W, col, res);
+#pragma unroll
+                for (int e = 0; e < 3; ++e) gt[e][j] = res[e];
+            }
+        } else if constexpr (BALL) {
             // columns 0..2: W^-1 (-e_{j+1}); column 3: W^-1 (-R e_0); extras: W^-1 (0, X_i)
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
@@ -812,8 +886,8 @@ struct Solver {
         }
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
-            const double* p = v + OR + 4 * b;
-            const double res = p[0] - sqrt(p[1] * p[1] + p[2] * p[2] + p[3] * p[3]);
+            const double* p = v + OR + SD * b;
+            const double res = p[0] - sqrt(tail_dot<SD>(p, p));
             socv = (vs[b] & (res <= 0.0)) ? fmax(socv, -res) : socv;
         }
         any = R::max(any);
@@ -827,7 +901,7 @@ struct Solver {
 #pragma unroll
             for (int k = 0; k < OR; ++k) v[k] = vort(k) ? v[k] + sh : v[k];
 #pragma unroll
-            for (int b = 0; b < SS; ++b) v[OR + 4 * b] = vs[b] ? v[OR + 4 * b] + sh : v[OR + 4 * b];
+            for (int b = 0; b < SS; ++b) v[OR + SD * b] = vs[b] ? v[OR + SD * b] + sh : v[OR + SD * b];
         }
     }
 
@@ -852,7 +926,7 @@ struct Solver {
         if constexpr (BALL) {                      // the ball rows' products, zeros dropped
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
-                const int k0 = OR + 4 * b;
+                const int k0 = OR + SD * b;
                 soc_gtv(b, r + k0, gth);
                 H[3][3] = fma(sR[b], sR[b], H[3][3]);
 #pragma unroll
@@ -868,6 +942,23 @@ struct Solver {
 #pragma unroll
                         for (int k = 0; k < 3; ++k) H[4 + i][4 + i2] = fma(sX[b][k][i], sX[b][k][i2], H[4 + i][4 + i2]);
             }
+        }
+        if constexpr (CONE) {                      // the cone rows, same order as dense rows
+#pragma unroll
+            for (int b = 0; b < SS; ++b)
+#pragma unroll
+                for (int e = 0; e < 3; ++e) {
+                    const int k = OR + SD * b + e;
+                    double g[4] = {cq[b][e][0], cq[b][e][1], cq[b][e][2], (e == 0) ? cc0[b] : 0.0};
+#pragma unroll
+                    for (int j = 0; j < N; ++j) {
+                        if (j == 3 && e != 0) continue;
+                        gth[j] += g[j] * r[k];
+#pragma unroll
+                        for (int c = j; c < N; ++c)
+                            if (!(c == 3 && e != 0)) H[j][c] += g[j] * g[c];
+                    }
+                }
         }
         allsum_sym(H);
         allsum_vec(gth);
@@ -897,7 +988,7 @@ struct Solver {
 #pragma unroll
         for (int k = 0; k < M; ++k) {
             const bool v = vrow(k);
-            const double one = (k < OR || ((k - OR) & 3) == 0) ? 1.0 : 0.0;   // inert: e
+            const double one = (k < OR || ((k - OR) % SD) == 0) ? 1.0 : 0.0;   // inert: e
             s[k] = v ? t[k] : one;
             z[k] = v ? zt[k] : one;
         }
@@ -916,8 +1007,8 @@ struct Solver {
 
     struct SocState {
         SocNT W;
-        double lam[4];
-        double ll[4];
+        double lam[SD];
+        double ll[SD];
     };
 
     // -------- solve_lp_pdip, pdip.py:373-470 -------------------------------------------
@@ -952,8 +1043,8 @@ struct Solver {
             }
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
-                const int k0 = OR + 4 * b;
-                const double szb = s[k0] * z[k0] + s[k0 + 1] * z[k0 + 1] + s[k0 + 2] * z[k0 + 2] + s[k0 + 3] * z[k0 + 3];
+                const int k0 = OR + SD * b;
+                const double szb = full_dot<SD>(s + k0, z + k0);
                 sz = vs[b] ? sz + szb : sz;
             }
             sz = R::sum(sz);
@@ -986,18 +1077,18 @@ struct Solver {
             }
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
-                const int k0 = OR + 4 * b;
-                soc_nt(s + k0, z + k0, so[b].W);
-                soc_mul(so[b].W, z + k0, so[b].lam);
-                soc_prod(so[b].lam, so[b].lam, so[b].ll);
+                const int k0 = OR + SD * b;
+                soc_nt<SD>(s + k0, z + k0, so[b].W);
+                soc_mul<SD>(so[b].W, z + k0, so[b].lam);
+                soc_prod<SD>(so[b].lam, so[b].lam, so[b].ll);
             }
             // SOC part of the normal matrix
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
-                double gt[4][N];
+                double gt[SD][N];
                 soc_gtilde(b, so[b].W, gt);
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
+                for (int e = 0; e < SD; ++e)
 #pragma unroll
                     for (int j = 0; j < N; ++j)
 #pragma unroll
@@ -1019,7 +1110,7 @@ struct Solver {
 
             // ---- predictor (affine) direction
             double cp[M];                                // (W^-1 ds_a) o (W dz_a)
-            double dsS[SSA * 4], dzS[SSA * 4];           // SOC rows of the affine step
+            double dsS[SSA * SD], dzS[SSA * SD];         // SOC rows of the affine step
             double dx[N];
             double cmax = 1.0, p1 = 0.0, p2 = 0.0;
             predictor<FULL>(so, il, F, idg, dx, cp, dsS, dzS, cmax, p1, p2, dd);
@@ -1031,9 +1122,9 @@ struct Solver {
 #pragma unroll
             for (int b = 0; b < SS; ++b)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int k = OR + 4 * b + e;
-                    const double dsk = dsS[4 * b + e], dzk = dzS[4 * b + e];
+                for (int e = 0; e < SD; ++e) {
+                    const int k = OR + SD * b + e;
+                    const double dsk = dsS[SD * b + e], dzk = dzS[SD * b + e];
                     p1 = vs[b] ? fma(s[k], dzk, fma(z[k], dsk, p1)) : p1;
                     p2 = vs[b] ? fma(dsk, dzk, p2) : p2;
                 }
@@ -1042,17 +1133,17 @@ struct Solver {
             const double sigma = sc * sc * sc;                      // quirk Q6
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
-                const int k0 = OR + 4 * b;
-                double t1[4], t2[4];
-                soc_solve(so[b].W, dsS + 4 * b, t1);
-                soc_mul(so[b].W, dzS + 4 * b, t2);
-                soc_prod(t1, t2, cp + k0);
+                const int k0 = OR + SD * b;
+                double t1[SD], t2[SD];
+                soc_solve<SD>(so[b].W, dsS + SD * b, t1);
+                soc_mul<SD>(so[b].W, dzS + SD * b, t2);
+                soc_prod<SD>(t1, t2, cp + k0);
             }
 
             // ---- corrector (combined) direction; orthant G dx and dz are kept for the
             // update, ds (two adds) is recomputed there.
             const double smu = sigma * mu;
-            double sbzt[SSA][4], slds[SSA][4];
+            double sbzt[SSA][SD], slds[SSA][SD];
             DCOL_ISTAMP(it, 4);
             rhs_solve(so, il, F, idg, cp, smu, dx, sbzt, slds);
             DCOL_ISTAMP(it, 5);
@@ -1065,10 +1156,10 @@ struct Solver {
                 cmax = bound_inv(cmax, dsk, il[k]);
                 cmax = bound_inv(cmax, num, isz[k]);       // -dz / z = -num / (s z)
             }
-            double sdz[SSA][4], sds[SSA][4], su[SSA][4];
+            double sdz[SSA][SD], sds[SSA][SD], su[SSA][SD];
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
-                soc_step(so[b], OR + 4 * b, sbzt[b], slds[b], dx, su[b], sdz[b], sds[b]);
+                soc_step(so[b], OR + SD * b, sbzt[b], slds[b], dx, su[b], sdz[b], sds[b]);
                 cmax = soc_bound1(so[b].W, b, sds[b], sdz[b], cmax);
             }
             const double a = fmin(1.0, 0.99 * frcp1(R::max(cmax)));
@@ -1087,10 +1178,10 @@ struct Solver {
             }
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
-                const int k0 = OR + 4 * b;
+                const int k0 = OR + SD * b;
                 const double ab = vs[b] ? a : 0.0;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
+                for (int e = 0; e < SD; ++e) {
                     r[k0 + e] += a * su[b][e];
                     s[k0 + e] += ab * sds[b][e];
                     z[k0 + e] += ab * sdz[b][e];
@@ -1110,7 +1201,7 @@ struct Solver {
     // and on an orthant row (W^-1 b~z)_k - z_k = -(z (s + r) + smu - cp) / s  (one G'v pass
     // per right-hand side, no separate G'z accumulation).
     DCOL_HD void rhs_solve(const SocState* so, const double* il, const double (&F)[N][N], const double (&idg)[N],
-                           const double* cp, double smu, double* dx, double (*sbzt)[4], double (*slds)[4],
+                           const double* cp, double smu, double* dx, double (*sbzt)[SD], double (*slds)[SD],
                            const double* dd = nullptr) const {
         double rhs[N];
 #pragma unroll
@@ -1125,19 +1216,19 @@ struct Solver {
         }
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
-            const int k0 = OR + 4 * b;
+            const int k0 = OR + SD * b;
             // W^-1 b~z = W^-1 W^-1 (-rz - W lds) = -W^-2 (s + r) - W^-1 lds   (rz = s + G x - h)
             soc_lds(so[b], cp ? cp + k0 : nullptr, smu, slds[b]);
-            double m[4], sr[4], q[4];
-            soc_solve(so[b].W, slds[b], m);
+            double m[SD], sr[SD], q[SD];
+            soc_solve<SD>(so[b].W, slds[b], m);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) sr[e] = s[k0 + e] + r[k0 + e];
-            soc_w2inv(so[b].W, sr, q);
+            for (int e = 0; e < SD; ++e) sr[e] = s[k0 + e] + r[k0 + e];
+            soc_w2inv<SD>(so[b].W, sr, q);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) sbzt[b][e] = -q[e] - m[e];
-            double bz[4];
+            for (int e = 0; e < SD; ++e) sbzt[b][e] = -q[e] - m[e];
+            double bz[SD];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) bz[e] = sbzt[b][e] - z[k0 + e];
+            for (int e = 0; e < SD; ++e) bz[e] = sbzt[b][e] - z[k0 + e];
             soc_gtv(b, bz, rhs);
         }
         allsum_vec(rhs);
@@ -1159,12 +1250,12 @@ struct Solver {
     // ds = W(lds - W dz) = -(s + r) - u (the primal row of the Newton system)
     DCOL_HD void soc_step(const SocState& S, int k0, const double* wbz, const double* lds, const double* dx, double* u,
                           double* dz, double* ds) const {
-        double t[4];
+        double t[SD];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) u[e] = rowdot(k0 + e, dx);
-        soc_w2inv(S.W, u, t);
+        for (int e = 0; e < SD; ++e) u[e] = rowdot(k0 + e, dx);
+        soc_w2inv<SD>(S.W, u, t);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < SD; ++e) {
             dz[e] = t[e] - wbz[e];
             ds[e] = -(s[k0 + e] + r[k0 + e]) - u[e];
         }
@@ -1178,7 +1269,7 @@ struct Solver {
     DCOL_HD void predictor(const SocState* so, const double* il, const double (&F)[N][N], const double (&idg)[N],
                            double* dx, double* cp, double* dsS, double* dzS, double& cmax,
                            double& p1, double& p2, const double* dd = nullptr) const {
-        double sbzt[SSA][4], slds[SSA][4];
+        double sbzt[SSA][SD], slds[SSA][SD];
         rhs_solve(so, il, F, idg, nullptr, 0.0, dx, sbzt, slds, dd);
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
@@ -1196,8 +1287,8 @@ struct Solver {
         }
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
-            double u[4];
-            soc_step(so[b], OR + 4 * b, sbzt[b], slds[b], dx, u, dzS + 4 * b, dsS + 4 * b);
+            double u[SD];
+            soc_step(so[b], OR + SD * b, sbzt[b], slds[b], dx, u, dzS + SD * b, dsS + SD * b);
         }
     }
     // z v + (smu - cp) on the corrector, z v on the predictor
@@ -1207,24 +1298,24 @@ struct Solver {
     DCOL_HD static void soc_lds(const SocState& S, const double* cp, double smu, double* out) {
         if (!cp) {                               // lambda \ (-lambda o lambda) = -lambda
 #pragma unroll
-            for (int e = 0; e < 4; ++e) out[e] = -S.lam[e];
+            for (int e = 0; e < SD; ++e) out[e] = -S.lam[e];
             return;
         }
-        double v[4];
+        double v[SD];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = -S.ll[e] - (cp ? cp[e] : 0.0);
+        for (int e = 0; e < SD; ++e) v[e] = -S.ll[e] - (cp ? cp[e] : 0.0);
         if (cp) v[0] += smu;
-        soc_iprod(S.lam, v, out);
+        soc_iprod<SD>(S.lam, v, out);
     }
     // SOC part of the step bound (soc_linesearch over the lane's blocks; ds/dz hold the
     // SOC rows only), as a running max of inverse bounds like the orthant's cmax
     DCOL_HD void soc_bound(const SocState* so, const double* ds, const double* dz, double& cmax) const {
 #pragma unroll
-        for (int b = 0; b < SS; ++b) cmax = soc_bound1(so[b].W, b, ds + 4 * b, dz + 4 * b, cmax);
+        for (int b = 0; b < SS; ++b) cmax = soc_bound1(so[b].W, b, ds + SD * b, dz + SD * b, cmax);
     }
     DCOL_HD double soc_bound1(const SocNT& W, int b, const double* ds, const double* dz, double cmax) const {
-        const int k0 = OR + 4 * b;
-        const double ib = fmax(soc_ls_inv(s + k0, ds, W.lis[0], W.lrc[0]), soc_ls_inv(z + k0, dz, W.lis[1], W.lrc[1]));
+        const int k0 = OR + SD * b;
+        const double ib = fmax(soc_ls_inv<SD>(s + k0, ds, W.lis[0], W.lrc[0]), soc_ls_inv<SD>(z + k0, dz, W.lis[1], W.lrc[1]));
         return vs[b] ? fmax(cmax, ib) : cmax;
     }
 
@@ -1263,13 +1354,18 @@ struct Solver {
         for (int b = 0; b < SS; ++b) {
             const bool own = vs[b] && soc_owner[b] == prim;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const double ze = own ? z[OR + 4 * b + e] : 0.0;
+            for (int e = 0; e < SD; ++e) {
+                const double ze = own ? z[OR + SD * b + e] : 0.0;
                 g.zs[e] = own ? ze : g.zs[e];
-                if constexpr (!BALL) {
+                if constexpr (CONE) {
+                    if (e < 3) {                                          // cone rows: Qe(-E e_k)
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) g.u[c] = fma(ze, cq[b][e][c], g.u[c]);
+                    }
+                } else if constexpr (!BALL) {
                     const double zc = (g.kind == SOC_CONE) ? ze : 0.0;   // cone rows: Qe(-E e_k)
 #pragma unroll
-                    for (int c = 0; c < 3; ++c) g.u[c] = fma(zc, G[OR + 4 * b + e][c], g.u[c]);
+                    for (int c = 0; c < 3; ++c) g.u[c] = fma(zc, G[OR + SD * b + e][c], g.u[c]);
                 }
             }
         }
@@ -1409,7 +1505,7 @@ DCOL_HD void launder(P& p) {
 // FULL: every pair of the launch has o == OMAX (no padding rows); BALL: every SOC block of
 // the launch is a ball block (Solver).  The host picks the variant per launch
 // (dcol_capi.cpp: bucket_pairs).
-template <int N, int NSOC, int OMAX, int LPP, bool FULL = false, bool BALL = false>
+template <int N, int NSOC, int OMAX, int LPP, bool FULL = false, bool BALL = false, bool CONE = false>
 DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
     DCOL_STAMP(A, pi, q, 0);
     const int64_t B = A.B;
@@ -1427,7 +1523,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
     make_frame(S2, th2, F2);
     DCOL_STAMP(A, pi, q, 1);
 
-    Solver<N, NSOC, OMAX, LPP, BALL> P;
+    Solver<N, NSOC, OMAX, LPP, BALL, CONE> P;
     P.q = q;
 #ifdef DCOL_STAMPS
     P.dbg = (q == 0) ? A.stamps + 16 * pi + 8 : nullptr;
@@ -1468,7 +1564,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
             // lane differentiates one primitive: lane q takes primitive q & 1, so a 2+-lane
             // group does the two 6-coordinate gradients side by side instead of both in
             // every lane (a 1-lane group does both in turn)
-            using Agg = typename Solver<N, NSOC, OMAX, LPP, BALL>::LagAgg;
+            using Agg = typename Solver<N, NSOC, OMAX, LPP, BALL, CONE>::LagAgg;
             const Agg ag0 = P.lag_aggregate(T1, 0);
             const Agg ag1 = P.lag_aggregate(T2, 1);
             constexpr int NP = LPP >= 2 ? 1 : 2;
@@ -1529,7 +1625,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
 constexpr int kSolveBlock = DCOL_BLOCK;
 static_assert(kSolveBlock % 64 == 0, "one or more whole waves per workgroup");
 
-// FL: variant flags, bit 0 FULL, bit 1 BALL (variants.py)
+// FL: variant flags, bit 0 FULL, bit 1 BALL, bit 2 CONE (variants.py)
 template <int N, int NSOC, int OMAX, int LPP, int WPS, int FL>
 __global__ void __launch_bounds__(kSolveBlock, WPS) prox_kernel(KArgs A) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1537,7 +1633,7 @@ __global__ void __launch_bounds__(kSolveBlock, WPS) prox_kernel(KArgs A) {
     const int q = (int)(t % LPP);
     if (slot >= A.n) return;
     const int64_t pi = A.perm ? (int64_t)A.perm[A.slot0 + slot] : (A.slot0 + slot);
-    solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0>(A, pi, q);
+    solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0>(A, pi, q);
 }
 
 }  // namespace dcol

@@ -6,7 +6,7 @@
 // launches spread over streams cost more in launch, fork and join latency than the solves
 // themselves.  Here each workgroup finds its bucket in a small segment table (scalar loads,
 // uniform per workgroup) and switches on the bucket's variant id to the same
-// solve_one<N, NSOC, OMAX, LPP, FULL, BALL> the per-variant kernels run, with that shape's
+// solve_one<N, NSOC, OMAX, LPP, FULL, BALL, CONE> the per-variant kernels run, with that shape's
 // latency configuration (largest LPP; csrc/variants.py fused()).  One wave per workgroup, so
 // a wave never mixes variants and never diverges on structure.
 #include "dcol_device.hpp"
@@ -28,7 +28,7 @@ __global__ void __launch_bounds__(kSolveBlock, 1) prox_fused_kernel(KArgs A, con
     switch (S.vid) {
 #define DCOL_FCASE(ID, NN, NS, OM, LP, FL)                  \
     case ID:                                                \
-        solve_one<NN, NS, OM, LP, (FL & 1) != 0, (FL & 2) != 0>(A, pi, q); \
+        solve_one<NN, NS, OM, LP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0>(A, pi, q); \
         break;
         DCOL_FUSED_VARIANTS(DCOL_FCASE)
 #undef DCOL_FCASE
@@ -38,9 +38,10 @@ __global__ void __launch_bounds__(kSolveBlock, 1) prox_fused_kernel(KArgs A, con
 }
 
 // (a bucket whose pairs all fill OMAX takes the padding-free case if there is one, a bucket
-// of ball-SOC pairs the structured case, else the plain one -- as the per-variant launchers do)
+// of ball-SOC or cone-SOC pairs the structured case, else the plain one -- as the
+// per-variant launchers do)
 int fused_vid(int N, int nsoc, int omax, int lpp, int flags) {
-    for (const int want : {(int)LF_FULL, (int)LF_BALL, 0}) {
+    for (const int want : {(int)LF_FULL, (int)LF_BALL, (int)LF_CONE, 0}) {
         if ((want & flags) != want) continue;
 #define DCOL_FID(ID, NN, NS, OM, LP, FL) \
     if (NN == N && NS == nsoc && OM == omax && LP == lpp && FL == want) return ID;

@@ -25,6 +25,10 @@ polygon -- no cone) runs a copy of the kernel that holds those blocks in structu
 (radius + extra columns instead of 4 dense G rows; dcol_device.hpp Solver<..., BALL>).
 Built for every SOC shape with N <= 6; the host buckets cone pairs apart.
 
+CONE variants: a launch whose SOC blocks are all cone blocks (polytope x cone, cone x cone;
+N = 4) runs a copy that holds each cone block as its 3 x 3 rotation part plus the row-0
+column-3 constant, unpadded (3-dim SOC arithmetic; dcol_device.hpp Solver<..., CONE>).
+
 FUSED variants: one launch for a whole small plan.  A plan that mixes several variants
 and cannot fill the GPU (an ALTRO phase: one victim against spheres, capsules, cylinders,
 cones and polytopes) runs every bucket in ONE launch of prox_fused_kernel, whose
@@ -32,10 +36,11 @@ workgroups switch on a per-segment variant id (dcol_kernels_fused.hip) — no st
 one launch latency.  Each shape's latency configuration (largest LPP) is in the switch,
 plus the padding-free copies of the FULL shapes; case-4 shapes (N = 7, 8) are not.
 
-Generates dcol_variants.inc (FL = variant flags: bit 0 FULL, bit 1 BALL):
+Generates dcol_variants.inc (FL = variant flags: bit 0 FULL, bit 1 BALL, bit 2 CONE):
   DCOL_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, 0) for every compiled kernel
   DCOL_FULL_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, 1) for the padding-free copies
   DCOL_BALL_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, 2) for the ball-SOC copies
+  DCOL_CONE_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, 4) for the structured-cone copies
   DCOL_SHAPES(X)    X(N, NSOC, OMAX) once per shape (used by the test emulator)
   DCOL_FUSED_VARIANTS(X)  X(ID, N, NSOC, OMAX, LPP, FL) the cases of the fused kernel
 """
@@ -88,6 +93,12 @@ def ball(n, nsoc):
     return nsoc >= 1 and n <= 6
 
 
+def cone(n, nsoc, omax=0):
+    """shapes with structured-cone copies (see module docstring); the many-faced buckets
+    above FUSE_OMAX keep the dense rows only (compile time; rare pairs)"""
+    return nsoc >= 1 and n == 4 and omax <= FUSE_OMAX
+
+
 # (N, NSOC, OMAX, LPP) configurations without a ball copy.  Empty: the (6, 1, 12) ball
 # kernel at LPP 2 was excluded once (commit 326f844: alpha 3e-10 / gradient 2e-5 off the C
 # oracle on polygon-first x box pairs); that drift was a machine-code defect of that one
@@ -128,6 +139,8 @@ def fused():
                 out.append((n, s, o, lpp, 1))
             if ball(n, s) and (n, s, o, lpp) not in BALL_SKIP:
                 out.append((n, s, o, lpp, 2))
+            if cone(n, s, o):
+                out.append((n, s, o, lpp, 4))
     return out
 
 
@@ -141,6 +154,8 @@ def main():
     lines += ["", "#define DCOL_BALL_VARIANTS(X) \\"]
     lines += [f"    X({n}, {s}, {o}, {l}, {w}, 2) \\" for n, s, o in shapes if ball(n, s) for l, w in configs(n, s, o)
               if (n, s, o, l) not in BALL_SKIP]
+    lines += ["", "#define DCOL_CONE_VARIANTS(X) \\"]
+    lines += [f"    X({n}, {s}, {o}, {l}, {w}, 4) \\" for n, s, o in shapes if cone(n, s, o) for l, w in configs(n, s, o)]
     lines += ["", "#define DCOL_SHAPES(X) \\"]
     lines += [f"    X({n}, {s}, {o}) \\" for n, s, o in shapes]
     lines += ["", "#define DCOL_FUSED_VARIANTS(X) \\"]

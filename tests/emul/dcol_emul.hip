@@ -46,6 +46,7 @@ extern "C" int dcol_emul_batch(const dcol_shape_desc* shapes, int32_t n, int64_t
     A.iters = iters;
     A.status = status;
     const bool no_ball = std::getenv("DCOL_NO_BALL") != nullptr;
+    const bool no_cone = std::getenv("DCOL_NO_CONE") != nullptr;
     for (int64_t i = 0; i < B; ++i) {
         PairClass c = classify(sh[s1[i]], sh[s2[i]]);
         if (c.status != DCOL_OK) {
@@ -59,13 +60,16 @@ extern "C" int dcol_emul_batch(const dcol_shape_desc* shapes, int32_t n, int64_t
         const bool full = c.o == c.omax;   // both loop specialisations, as the GPU launches pick them
         // ball-SOC specialisation as the GPU plans pick it (DCOL_NO_BALL: the dense rows)
         const bool ball = c.nsoc > 0 && sh[s1[i]].soc_kind != SOC_CONE && sh[s2[i]].soc_kind != SOC_CONE && !no_ball;
+        // structured-cone specialisation (N = 4, every SOC block a cone; DCOL_NO_CONE: dense)
+        const bool cone = c.nsoc > 0 && c.N == 4 && sh[s1[i]].soc_kind != SOC_BALL && sh[s2[i]].soc_kind != SOC_BALL &&
+                          !no_cone;
         bool done = false;
         switch (c.N) {
-            case 4: done = emul::solve_n<4>(c, full, ball, A, i); break;
-            case 5: done = emul::solve_n<5>(c, full, ball, A, i); break;
-            case 6: done = emul::solve_n<6>(c, full, ball, A, i); break;
-            case 7: done = emul::solve_n<7>(c, full, ball, A, i); break;
-            case 8: done = emul::solve_n<8>(c, full, ball, A, i); break;
+            case 4: done = emul::solve_n<4>(c, full, ball, cone, A, i); break;
+            case 5: done = emul::solve_n<5>(c, full, ball, cone, A, i); break;
+            case 6: done = emul::solve_n<6>(c, full, ball, cone, A, i); break;
+            case 7: done = emul::solve_n<7>(c, full, ball, cone, A, i); break;
+            case 8: done = emul::solve_n<8>(c, full, ball, cone, A, i); break;
             default: break;
         }
         if (done) continue;

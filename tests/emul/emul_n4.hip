@@ -1,4 +1,4 @@
 // TEST-ONLY (tests/emul): x86 solver variants with N = 4
 #include "emul_solve.hpp"
 
-template bool emul::solve_n<4>(const dcol_host::PairClass&, bool, bool, const dcol::KArgs&, int64_t);
+template bool emul::solve_n<4>(const dcol_host::PairClass&, bool, bool, bool, const dcol::KArgs&, int64_t);

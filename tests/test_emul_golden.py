@@ -34,16 +34,18 @@ def emul(d, tol, flags, max_iter=50):
     return al, ct, gr, it, st
 
 
-@pytest.mark.parametrize("soc_rows", ["ball", "dense"])
+@pytest.mark.parametrize("soc_rows", ["structured", "dense"])
 @pytest.mark.parametrize("flags", [1 | 4, 2 | 4], ids=["fd", "envelope"])
 @pytest.mark.parametrize("path", [p for p in golden_files() if "tol0" not in p], ids=lambda p: p.split("/")[-1][:-4])
 def test_emulated_kernel_matches_reference(path, flags, soc_rows, monkeypatch):
-    """Both SOC row forms: structured ball blocks (Solver<..., BALL>, what plans of cone-free
-    SOC pairs run) and the dense rows (DCOL_NO_BALL)."""
-    if soc_rows == "dense":
-        monkeypatch.setenv("DCOL_NO_BALL", "1")
-    else:
-        monkeypatch.delenv("DCOL_NO_BALL", raising=False)
+    """Both SOC row forms: structured blocks (Solver<..., BALL> for cone-free SOC pairs,
+    Solver<..., CONE> for ball-free N = 4 pairs -- what the GPU plans run) and the dense rows
+    (DCOL_NO_BALL, DCOL_NO_CONE)."""
+    for var in ("DCOL_NO_BALL", "DCOL_NO_CONE"):
+        if soc_rows == "dense":
+            monkeypatch.setenv(var, "1")
+        else:
+            monkeypatch.delenv(var, raising=False)
     d = load_golden(path)
     al, ct, gr, it, st = emul(d, float(d["tol"]), flags)
     np.testing.assert_array_equal(st, d["status"])

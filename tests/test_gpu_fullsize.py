@@ -186,6 +186,38 @@ np.savez(sys.argv[1], alpha=r.alpha, grad=r.grad, contact=r.contact, iters=r.ite
 """
 
 
+def _mixed_outputs(tmp_path, name, lib=None, env_extra=None):
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    for k in ("DCOL_LIB", "DCOL_NO_BALL", "DCOL_NO_CONE", "DCOL_LPP"):
+        env.pop(k, None)
+    if lib:
+        env["DCOL_LIB"] = lib
+    env.update(env_extra or {})
+    f = str(tmp_path / f"{name}.npz")
+    subprocess.run([sys.executable, "-c", _SOLVE_SCRIPT, f, PKG, REPO], check=True, env=env, timeout=300)
+    return dict(np.load(f))
+
+
+def _assert_bitwise(a, b):
+    for k in ("status", "iters"):
+        np.testing.assert_array_equal(a[k], b[k])
+    for k in ("alpha", "grad", "contact", "genv"):
+        same = (a[k] == b[k]) | (np.isnan(a[k]) & np.isnan(b[k]))
+        assert same.all(), (k, int((~same).sum()))
+
+
+def test_structured_cone_rows_equal_dense(tmp_path):
+    """The CONE kernels (cone blocks as 3 x 3 rotation part + one constant, 3-dim SOC
+    arithmetic, no zero padding) compute the dense padded kernels' nonzero terms in the same
+    order: bitwise equal over the 1M mixed workload (polytope x cone, cone x polytope and
+    cone x cone are the classes that switch kernels; DCOL_NO_CONE=1 keeps the dense rows)."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    _assert_bitwise(_mixed_outputs(tmp_path, "structured"), _mixed_outputs(tmp_path, "dense", env_extra={"DCOL_NO_CONE": "1"}))
+
+
 @pytest.mark.skipif(not os.path.exists(XCHECK_LIB), reason="lib_xcheck not built (make -C csrc xcheck)")
 def test_codegen_invariance_mixed(tmp_path):
     """The product library and its twin built from the same sources with another machine
@@ -194,20 +226,4 @@ def test_codegen_invariance_mixed(tmp_path):
     modes, contact points): FP semantics are fixed in the IR before scheduling, so any
     difference is a machine-code defect -- the class of fault that made the 326f844 build
     of the (6, 1, 12) LPP-2 ball kernel drift."""
-    import subprocess
-    import sys
-    outs = []
-    for name, lib in (("product", None), ("xcheck", XCHECK_LIB)):
-        env = dict(os.environ)
-        env.pop("DCOL_LIB", None)
-        if lib:
-            env["DCOL_LIB"] = lib
-        f = str(tmp_path / f"{name}.npz")
-        subprocess.run([sys.executable, "-c", _SOLVE_SCRIPT, f, PKG, REPO], check=True, env=env, timeout=300)
-        outs.append(dict(np.load(f)))
-    a, b = outs
-    for k in ("status", "iters"):
-        np.testing.assert_array_equal(a[k], b[k])
-    for k in ("alpha", "grad", "contact", "genv"):
-        same = (a[k] == b[k]) | (np.isnan(a[k]) & np.isnan(b[k]))
-        assert same.all(), (k, int((~same).sum()))
+    _assert_bitwise(_mixed_outputs(tmp_path, "product"), _mixed_outputs(tmp_path, "xcheck", lib=XCHECK_LIB))

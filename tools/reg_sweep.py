@@ -25,17 +25,19 @@ __global__ void __launch_bounds__(64, {w}) kb(KArgs A) {{
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t slot = t / LP; const int q = (int)(t % LP);
     if (slot >= A.n) return;
-    solve_one<N, NS, OM, LP, false>(A, slot, q);
+    solve_one<N, NS, OM, LP, false, {ball}, {cone}>(A, slot, q);
 }}
 template __global__ void kb<{n},{s},{o},{l}>(KArgs); }}
 """
 
 
 def run(job, tmp):
-    n, s, o, lpp, w = job
-    fn = os.path.join(tmp, f"k_{n}_{s}_{o}_{lpp}_{w}.hip")
-    open(fn, "w").write(SRC.format(n=n, s=s, o=o, l=lpp, w=w))
-    err = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{CSRC}", "-c", fn, "-o", os.devnull,
+    n, s, o, lpp, w, ball = job
+    fn = os.path.join(tmp, f"k_{n}_{s}_{o}_{lpp}_{w}_{ball}.hip")
+    open(fn, "w").write(SRC.format(n=n, s=s, o=o, l=lpp, w=w, ball="true" if ball == "ball" else "false",
+                                   cone="true" if ball == "cone" else "false"))
+    err = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=on", f"-I{CSRC}", "-c",
+                          fn, "-o", os.devnull,
                           "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True).stderr
     last = lambda pat: (re.findall(pat, err) or ["?"])[-1]  # noqa: E731
     return job, last(r"VGPRs: (\d+)"), last(r"AGPRs: (\d+)"), last(r"ScratchSize \[bytes/lane\]: (\d+)"), \
@@ -45,9 +47,17 @@ def run(job, tmp):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("-j", type=int, default=8)
+    ap.add_argument("--shapes", default="", help="comma-separated N:NSOC:OMAX list (default: every shape)")
+    ap.add_argument("--lpp", default="2,4,8")
+    ap.add_argument("--ball", action="store_true", help="the ball-SOC copies (Solver<..., BALL>)")
+    ap.add_argument("--cone", action="store_true", help="the structured cone copies (Solver<..., CONE>, N = 4)")
     args = ap.parse_args()
     shapes = [(n, s, o) for (n, s), os_ in sorted(variants.OMAX.items()) for o in os_]
-    jobs = [(n, s, o, l, w) for n, s, o in shapes for l in (2, 4, 8) if o % l == 0 for w in (1, 2)]
+    if args.shapes:
+        shapes = [tuple(int(v) for v in t.split(":")) for t in args.shapes.split(",")]
+    lpps = [int(v) for v in args.lpp.split(",")]
+    kind = "ball" if args.ball else ("cone" if args.cone else "")
+    jobs = [(n, s, o, l, w, kind) for n, s, o in shapes for l in lpps if o % l == 0 for w in (1, 2)]
     with tempfile.TemporaryDirectory() as tmp, ThreadPoolExecutor(args.j) as ex:
         for job, v, a, sc, oc in ex.map(lambda j: run(j, tmp), jobs):
             print(*job, "vgpr", v, "agpr", a, "scratch", sc, "occ", oc, flush=True)
