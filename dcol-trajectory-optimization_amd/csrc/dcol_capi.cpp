@@ -65,7 +65,7 @@ __global__ void __launch_bounds__(256) reject_kernel(KArgs A, int32_t code) {
     if (A.status) A.status[pi] = code;
     if ((A.flags & F_CONTACT) && A.contact)
         for (int q = 0; q < 3; ++q) A.contact[q * B + pi] = nan;
-    if ((A.flags & (F_GRAD_FD | F_GRAD_ENV)) && A.grad)
+    if ((A.flags & (F_GRAD_FD | F_GRAD_ENV | F_GRAD_IMP)) && A.grad)
         for (int q = 0; q < 12; ++q) A.grad[q * B + pi] = nan;
 }
 
@@ -531,7 +531,7 @@ int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, 
     if (p->B == 0) return DCOL_SUCCESS;
     if (!pose1 || !pose2 || !alpha) return fail(DCOL_ERR_ARG, "dcol_plan_run: pose1, pose2 and alpha are required");
     if ((flags & DCOL_CONTACT) && !contact) return fail(DCOL_ERR_ARG, "dcol_plan_run: DCOL_CONTACT needs contact[]");
-    if ((flags & (DCOL_GRAD_FD | DCOL_GRAD_ENVELOPE)) && !grad) return fail(DCOL_ERR_ARG, "dcol_plan_run: gradient flag needs grad[]");
+    if ((flags & DCOL_GRAD_ANY) && !grad) return fail(DCOL_ERR_ARG, "dcol_plan_run: gradient flag needs grad[]");
     if (max_iter < 0) return fail(DCOL_ERR_ARG, "dcol_plan_run: max_iter < 0");
     const dcol_table* t = p->table;
     DeviceGuard g(t->device);
@@ -671,7 +671,7 @@ int dcol_prox_batch_host(const dcol_table* tc, int64_t B, const int32_t* s1, con
     if (contact && (flags & DCOL_CONTACT))
         for (int64_t i = 0; i < B; ++i)
             for (int q = 0; q < 3; ++q) contact[3 * i + q] = outd[(size_t)B + q * B + i];
-    if (grad && (flags & (DCOL_GRAD_FD | DCOL_GRAD_ENVELOPE)))
+    if (grad && (flags & DCOL_GRAD_ANY))
         for (int64_t i = 0; i < B; ++i)
             for (int q = 0; q < 12; ++q) grad[12 * i + q] = outd[(size_t)4 * B + q * B + i];
     return DCOL_SUCCESS;
@@ -811,11 +811,11 @@ int dcol_prox_batch_multi_gpu(const dcol_plan* p, dcol_comm* c, const double* po
         return fail(DCOL_ERR_ARG, "dcol_prox_batch_multi_gpu: plan and communicator on different devices");
     const int32_t rflags = flags & ~DCOL_CONTACT;   // the record carries no contact point
     int rc = dcol_plan_run(p, pose1, pose2, tol, max_iter, rflags, alpha, nullptr,
-                           (rflags & (DCOL_GRAD_FD | DCOL_GRAD_ENVELOPE)) ? grad : nullptr, iters, status, stream);
+                           (rflags & DCOL_GRAD_ANY) ? grad : nullptr, iters, status, stream);
     if (rc != DCOL_SUCCESS) return rc;
     DeviceGuard g(c->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const bool want_grad = (rflags & (DCOL_GRAD_FD | DCOL_GRAD_ENVELOPE)) && grad;
+    const bool want_grad = (rflags & DCOL_GRAD_ANY) && grad;
     if (cap > 0) {
         const int64_t grid = (cap + kPackRows - 1) / kPackRows;
         hipLaunchKernelGGL(pack_records, dim3(grid), dim3(kPackRows), 0, st, p->B, cap, alpha, want_grad ? grad : nullptr,

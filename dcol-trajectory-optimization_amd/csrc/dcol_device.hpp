@@ -96,7 +96,7 @@ DCOL_HD bool pos_finite(double x) {
 
 enum : int32_t { ST_OK = 0, ST_MAXITER = 1, ST_UNSUPPORTED = 2, ST_NOT_PD = 3, ST_NONFINITE = 4, ST_TOO_LARGE = 5 };
 enum : int32_t { SOC_NONE = 0, SOC_BALL = 1, SOC_CONE = 2 };
-enum : int32_t { F_GRAD_FD = 1, F_GRAD_ENV = 2, F_CONTACT = 4 };
+enum : int32_t { F_GRAD_FD = 1, F_GRAD_ENV = 2, F_CONTACT = 4, F_GRAD_IMP = 16 };
 
 // One primitive, pre-digested on the host (dcol_capi.cpp: digest_shape()).
 struct DevShape {
@@ -562,6 +562,7 @@ struct Solver {
     double cq[SSA][3][3], cc0[SSA];             // CONE: row e of slot b = [cq[b][e] | e == 0 ? cc0[b] : 0]
     double s[M], z[M], r[M];   // slack, dual, primal residual G x - h
     double x[N];
+    double vimp[N];            // implicit-gradient mode: H^-1 e3 at the returned iterate
     int q, o1, o, deg;
     int xo2;                   // first extra column of primitive 2 minus 4: S1.n_extra for a
                                // case-4 pair (both primitives have extras; opt-in extension),
@@ -1339,14 +1340,15 @@ struct Solver {
         double zs[4];    // the primitive's SOC block duals (zero if none), group-summed
         int kind;        // SOC kind of the primitive's block
     };
-    DCOL_HD LagAgg lag_aggregate(const DevShape& S, int prim) const {
+    // wt: per-row weights replacing z (the implicit mode's -W^-2 G v), nullptr = z
+    DCOL_HD LagAgg lag_aggregate(const DevShape& S, int prim, const double* wt = nullptr) const {
         LagAgg g;
         g.u[0] = g.u[1] = g.u[2] = 0.0;
         g.zs[0] = g.zs[1] = g.zs[2] = g.zs[3] = 0.0;
         g.kind = S.soc_kind;
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
-            const double zk = owns_row(k, prim) ? z[k] : 0.0;
+            const double zk = owns_row(k, prim) ? (wt ? wt[k] : z[k]) : 0.0;
 #pragma unroll
             for (int c = 0; c < 3; ++c) g.u[c] = fma(zk, G[k][c], g.u[c]);
         }
@@ -1355,7 +1357,7 @@ struct Solver {
             const bool own = vs[b] && soc_owner[b] == prim;
 #pragma unroll
             for (int e = 0; e < SD; ++e) {
-                const double ze = own ? z[OR + SD * b + e] : 0.0;
+                const double ze = own ? (wt ? wt[OR + SD * b + e] : z[OR + SD * b + e]) : 0.0;
                 g.zs[e] = own ? ze : g.zs[e];
                 if constexpr (CONE) {
                     if (e < 3) {                                          // cone rows: Qe(-E e_k)
@@ -1487,6 +1489,108 @@ struct Solver {
             g[3 + j] = acc;
         }
     }
+
+    // -------- implicit-function gradient (DCOL_GRAD_IMPLICIT) --------------------------
+    // The KKT system at the returned iterate, G'z + c = 0, G x + s = h, s o z = mu e,
+    // linearised in the pose with the NT scaling (ds = -W^2 dz, the PDIP's own Newton
+    // linearisation, pdip.py:424-460): H dx = -dG'z - G'W^-2 (dG x - dh), H = G'W^-2 G (the
+    // normal matrix G~'G~ of pdip.py:434), so with v = H^-1 e3
+    //   d alpha = e3'dx = sum_i a_i (dG_i x - dh_i) - z_i (dG_i v),   a = -W^-2 G v.
+    // Returns the per-row weights a (lane rows, like z) and v in vimp; false if the normal
+    // matrix at this iterate does not factor (the caller then uses the envelope form).
+    DCOL_HD bool implicit_weights(double* wts) {
+        double Hm[N][N], dd[OR > 0 ? OR : 1];
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+#pragma unroll
+            for (int c = j; c < N; ++c) Hm[j][c] = 0.0;
+#pragma unroll
+        for (int k = 0; k < OR; ++k) {
+            const double rsz = frcp1(s[k] * z[k]);
+            dd[k] = z[k] * (z[k] * rsz);                      // W^-2 = z / s
+            double g[N];
+#pragma unroll
+            for (int j = 0; j < N; ++j) g[j] = G[k][j] * dd[k];
+#pragma unroll
+            for (int j = 0; j < N; ++j)
+#pragma unroll
+                for (int c = j; c < N; ++c) Hm[j][c] += g[j] * G[k][c];
+        }
+        SocNT W[SSA];
+#pragma unroll
+        for (int b = 0; b < SS; ++b) {
+            soc_nt<SD>(s + OR + SD * b, z + OR + SD * b, W[b]);
+            double gt[SD][N];
+            soc_gtilde(b, W[b], gt);
+#pragma unroll
+            for (int e = 0; e < SD; ++e)
+#pragma unroll
+                for (int j = 0; j < N; ++j)
+#pragma unroll
+                    for (int c = j; c < N; ++c) Hm[j][c] += gt[e][j] * gt[e][c];
+        }
+        allsum_sym(Hm);
+        double F[N][N], idg[N], e3[N];
+        const bool fine = chol(Hm, F, idg);
+#pragma unroll
+        for (int j = 0; j < N; ++j) e3[j] = (j == 3) ? 1.0 : 0.0;
+        chol_solve(F, idg, e3, vimp);
+#pragma unroll
+        for (int k = 0; k < OR; ++k) wts[k] = -(dd[k] * rowdot(k, vimp));
+#pragma unroll
+        for (int b = 0; b < SS; ++b) {
+            const int k0 = OR + SD * b;
+            double u[SD], t[SD];
+#pragma unroll
+            for (int e = 0; e < SD; ++e) u[e] = rowdot(k0 + e, vimp);
+            soc_w2inv<SD>(W[b], u, t);
+#pragma unroll
+            for (int e = 0; e < SD; ++e) wts[k0 + e] = vs[b] ? -t[e] : 0.0;
+        }
+        return fine;
+    }
+    // d alpha / d theta_prim = E(agA; x) - E_G(agZ; v): E the envelope form of
+    // env_grad_prim with the weights a, E_G(z; v) = sum_i z_i dG_i v (dG only: no h term;
+    // zero for translations, v3' Q_j (Q_off w_z) + zeta_z' Q_j (Q_off xi_v) for rotations)
+    DCOL_HD void imp_grad_prim(const LagAgg& agA, const LagAgg& agZ, const DevShape& S, int prim, const double th[6],
+                               double* g) const {
+        env_grad_prim(agA, S, prim, th, g);
+        Frame Fr;
+        make_frame(S, th, Fr);
+        double w[3], zeta[3] = {0.0, 0.0, 0.0}, xi[3] = {0.0, 0.0, 0.0};
+        body_w(agZ, Fr, w);
+        if (agZ.kind == SOC_BALL) {
+            zeta[0] = agZ.zs[1]; zeta[1] = agZ.zs[2]; zeta[2] = agZ.zs[3];
+        }
+        if (S.soc_kind == SOC_BALL) {
+            const int off = xoff(prim == 1);
+#pragma unroll
+            for (int j = 4; j < N; ++j) {
+                if (S.n_extra >= 1 && j == 4 + off) xi[0] = vimp[j];
+                if (S.n_extra >= 2 && j == 5 + off) xi[1] = vimp[j];
+            }
+        }
+        double c1[3], c2[3];
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) {
+            c1[rr] = S.Q_off[3 * rr] * w[0] + S.Q_off[3 * rr + 1] * w[1] + S.Q_off[3 * rr + 2] * w[2];
+            c2[rr] = S.Q_off[3 * rr] * xi[0] + S.Q_off[3 * rr + 1] * xi[1] + S.Q_off[3 * rr + 2] * xi[2];
+        }
+        double dQ[3][9];
+        dcm_jacobian(th + 3, dQ);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            double acc = 0.0;
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) {
+                const double* qq = &dQ[j][3 * rr];
+                const double m1 = qq[0] * c1[0] + qq[1] * c1[1] + qq[2] * c1[2];
+                const double m3 = qq[0] * c2[0] + qq[1] * c2[1] + qq[2] * c2[2];
+                acc += vimp[rr] * m1 + zeta[rr] * m3;
+            }
+            g[3 + j] -= acc;
+        }
+    }
 };
 
 // ------------------------------------------------------------------------------------
@@ -1541,7 +1645,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
     const double nan = __builtin_nan("");
     const bool ok = st == ST_OK;
     double g[12];
-    const bool want_grad = (A.flags & (F_GRAD_FD | F_GRAD_ENV)) && A.grad;
+    const bool want_grad = (A.flags & (F_GRAD_FD | F_GRAD_ENV | F_GRAD_IMP)) && A.grad;
     if (want_grad) {
         // Phase boundary: make the gradient re-read poses, shape records and row descriptors
         // instead of keeping the assembly-phase copies live across the whole PDIP loop
@@ -1567,6 +1671,16 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
             using Agg = typename Solver<N, NSOC, OMAX, LPP, BALL, CONE>::LagAgg;
             const Agg ag0 = P.lag_aggregate(T1, 0);
             const Agg ag1 = P.lag_aggregate(T2, 1);
+            // implicit mode: weights a = -W^-2 G v at this iterate, aggregated like z
+            const bool imp = (A.flags & F_GRAD_IMP) != 0;
+            Agg agA0 = ag0, agA1 = ag1;
+            bool imp_ok = false;
+            if (imp) {
+                double wts[Solver<N, NSOC, OMAX, LPP, BALL, CONE>::M];
+                imp_ok = P.implicit_weights(wts);
+                agA0 = P.lag_aggregate(T1, 0, wts);
+                agA1 = P.lag_aggregate(T2, 1, wts);
+            }
             constexpr int NP = LPP >= 2 ? 1 : 2;
 #pragma unroll
             for (int pp = 0; pp < NP; ++pp) {
@@ -1582,8 +1696,19 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
 #pragma unroll
                 for (int c = 0; c < 6; ++c) th[c] = prim ? th2[c] : th1[c];
                 double* gp = g + 6 * pp;
-                if (A.flags & F_GRAD_ENV) P.env_grad_prim(ag, T, prim, th, gp);
-                else P.fd_grad_prim(ag, T, prim, th, gp);
+                if (imp && imp_ok) {
+                    Agg agA;
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) agA.u[c] = prim ? agA1.u[c] : agA0.u[c];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) agA.zs[c] = prim ? agA1.zs[c] : agA0.zs[c];
+                    agA.kind = ag.kind;
+                    P.imp_grad_prim(agA, ag, T, prim, th, gp);
+                } else if (A.flags & (F_GRAD_ENV | F_GRAD_IMP)) {
+                    P.env_grad_prim(ag, T, prim, th, gp);
+                } else {
+                    P.fd_grad_prim(ag, T, prim, th, gp);
+                }
             }
         } else {
 #pragma unroll

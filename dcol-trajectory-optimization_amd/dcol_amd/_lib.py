@@ -17,7 +17,8 @@ POLYTOPE, SPHERE, CONE, CAPSULE, CYLINDER, POLYGON = range(6)
 # enum dcol_status
 OK, MAXITER, UNSUPPORTED, NOT_PD, NONFINITE, TOO_LARGE = range(6)
 # enum dcol_flags
-GRAD_FD, GRAD_ENVELOPE, CONTACT, CASE4 = 1, 2, 4, 8
+GRAD_FD, GRAD_ENVELOPE, CONTACT, CASE4, GRAD_IMPLICIT = 1, 2, 4, 8, 16
+GRAD_ANY = GRAD_FD | GRAD_ENVELOPE | GRAD_IMPLICIT
 # enum dcol_plan_options
 PLAN_CASE4, PLAN_NO_FUSE = 1, 2
 SUCCESS, ERR_ARG, ERR_HIP, ERR_NOMEM = 0, -1, -2, -3

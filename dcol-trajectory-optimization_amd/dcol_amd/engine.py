@@ -42,7 +42,9 @@ def grad_flag(grad) -> int:
         return _lib.GRAD_FD
     if grad == "envelope":
         return _lib.GRAD_ENVELOPE
-    raise ValueError(f"grad must be None, 'fd' or 'envelope', got {grad!r}")
+    if grad == "implicit":
+        return _lib.GRAD_IMPLICIT
+    raise ValueError(f"grad must be None, 'fd', 'envelope' or 'implicit', got {grad!r}")
 
 
 def raise_for_status(status: int):
@@ -140,7 +142,7 @@ class Plan:
                 raise ValueError(f"poses must be contiguous float64 [6, {B}] on {dev}")
         flags = grad_flag(grad) | (_lib.CONTACT if contact else 0)
         if out is None:
-            out = alloc_outputs(B, dev, bool(flags & (_lib.GRAD_FD | _lib.GRAD_ENVELOPE)), bool(contact))
+            out = alloc_outputs(B, dev, bool(flags & _lib.GRAD_ANY), bool(contact))
         if stream is None:
             stream = torch.cuda.current_stream(dev)
         ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
@@ -162,7 +164,7 @@ class Plan:
             if t.dtype != torch.float64 or tuple(t.shape) != (6, B) or not t.is_contiguous() or t.device != dev:
                 raise ValueError(f"poses must be contiguous float64 [6, {B}] on {dev}")
         flags = grad_flag(grad) | (_lib.CONTACT if contact else 0)
-        if (flags & (_lib.GRAD_FD | _lib.GRAD_ENVELOPE)) and "grad" not in out:
+        if (flags & _lib.GRAD_ANY) and "grad" not in out:
             raise ValueError("out has no 'grad' buffer")
         if contact and "contact" not in out:
             raise ValueError("out has no 'contact' buffer")
@@ -285,7 +287,7 @@ class Engine:
         flags = grad_flag(grad) | (_lib.CONTACT if contact else 0) | (_lib.CASE4 if case4 else 0)
         alpha = np.empty(B)
         cp = np.empty((B, 3)) if contact else None
-        g = np.empty((B, 12)) if flags & (_lib.GRAD_FD | _lib.GRAD_ENVELOPE) else None
+        g = np.empty((B, 12)) if flags & _lib.GRAD_ANY else None
         iters = np.empty(B, dtype=np.int32)
         status = np.empty(B, dtype=np.int32)
         table = self.table

@@ -17,6 +17,8 @@ def proximity_gradient(prim1, prim2, pdip_tol=DEFAULT_TOL, verbose=False):
 
 def proximity_gradient_batch(prims1, prims2, pdip_tol=DEFAULT_TOL, grad="fd"):
     """Batched form -> (alpha [B], grad [B, 12], status [B]); grad = 'fd' (reference
-    mode) or 'envelope' (closed form)."""
+    mode), 'envelope' (closed form of the same derivative) or 'implicit' (implicit-function
+    derivative of the returned iterate through the PDIP's normal matrix; closer to the true
+    d alpha / d pose than the reference's formulation at the same tolerance)."""
     res = default_engine().solve_objects(prims1, prims2, tol=pdip_tol, grad=grad, contact=False)
     return res.alpha, res.grad, res.status

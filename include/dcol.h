@@ -64,9 +64,16 @@ enum dcol_flags {
                                proximity_gradient.py:50-88)                               */
     DCOL_GRAD_ENVELOPE = 2, /* the same gradient in closed form (envelope theorem)       */
     DCOL_CONTACT = 4,       /* write x[0:3] (proximity.py:51-54)                          */
-    DCOL_CASE4 = 8          /* dcol_prox_batch_host only: solve case-4 pairs (see
+    DCOL_CASE4 = 8,         /* dcol_prox_batch_host only: solve case-4 pairs (see
                                DCOL_PLAN_CASE4) instead of reporting DCOL_UNSUPPORTED     */
+    DCOL_GRAD_IMPLICIT = 16 /* implicit-function derivative of the returned iterate: the
+                               KKT system linearised with the NT scaling at (x, s, z),
+                               d alpha = e3' H^-1 (-dG'z - G'W^-2 (dG x - dh)) with H the
+                               PDIP's normal matrix G'W^-2 G (same Cholesky routine), for
+                               the 12 pose coordinates; equals the envelope gradient as
+                               mu -> 0 (pdip.py:434; no reference counterpart)            */
 };
+#define DCOL_GRAD_ANY (DCOL_GRAD_FD | DCOL_GRAD_ENVELOPE | DCOL_GRAD_IMPLICIT)
 
 /* dcol_plan_create_ex options. */
 enum dcol_plan_options {

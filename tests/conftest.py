@@ -20,8 +20,8 @@ for p in (PKG, REPO):
         sys.path.insert(0, p)
 
 # parity tolerances (north star: alpha 1e-6 rel, gradient 1e-5 rel; SURVEY.md §7: the
-# reference's own FD gradient is noisy at ~1e-7 of ||g||, so the gradient check is
-# norm-relative with a floor of 1, and alpha gets an absolute floor for alpha ~ 0)
+# reference's own FD gradient is noisy at ~1e-7 of ||g||, so the gradient check is relative
+# to ||g||_inf (floor 0.01), and alpha gets an absolute floor for alpha ~ 0)
 ALPHA_RTOL = 1e-6
 ALPHA_ATOL = 1e-12
 GRAD_TOL = 1e-5
@@ -44,8 +44,13 @@ def alpha_close(a, ref):
     return np.abs(a - ref) <= ALPHA_RTOL * np.abs(ref) + ALPHA_ATOL
 
 
+GRAD_FLOOR = 1e-2   # below ||g||_inf = 0.01 the bound is absolute (1e-7): the reference's own
+                    # FD noise on analytic zeros is ~3e-8
+
+
 def grad_close(g, ref):
-    return np.abs(g - ref).max(axis=-1) <= GRAD_TOL * np.maximum(np.abs(ref).max(axis=-1), 1.0)
+    """Gradient within 1e-5 of ||ref||_inf (north star: 1e-5 rel), floored at ||g|| = 0.01."""
+    return np.abs(g - ref).max(axis=-1) <= GRAD_TOL * np.maximum(np.abs(ref).max(axis=-1), GRAD_FLOOR)
 
 
 def gpu_available():

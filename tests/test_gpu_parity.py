@@ -28,8 +28,9 @@ def test_golden_parity(engine, path, mode):
     res = engine.solve_host(s1, s2, d["pose1"], d["pose2"], tol=float(d["tol"]), grad=mode if want_grad else None)
     np.testing.assert_array_equal(res.status, d["status"])
     ok = d["status"] == 0
-    # same iterate sequence as the reference (required for 1e-6 alpha parity)
-    assert np.mean(res.iters[ok] == d["iters"][ok]) >= 0.999, "iteration counts diverge from the reference"
+    # same iterate sequence as the reference (required for 1e-6 alpha parity):
+    # Newton iteration counts equal on every pair
+    np.testing.assert_array_equal(res.iters[ok], d["iters"][ok])
     assert np.all(alpha_close(res.alpha[ok], d["alpha"][ok]))
     assert np.all(np.abs(res.contact[ok] - d["contact"][ok]) <= 1e-6 * np.maximum(np.abs(d["contact"][ok]), 1.0))
     assert np.all(np.isnan(res.alpha[~ok]))
