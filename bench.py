@@ -495,12 +495,23 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
     launch = plan.bind(d1, d2, out, grad=args.grad, contact=False, stream=stream)
     n = len(mine)
     comm, path = None, "torch.distributed all_gather_into_tensor" if dist is not None else "local copy (world 1)"
+    native_error = None
     if args.backend == "nccl" and not args.torch_gather:
-        uid = [NativeComm.unique_id() if rank == 0 else None]
-        if dist is not None:
-            dist.broadcast_object_list(uid, src=0)
-        comm = NativeComm(uid[0], world, rank, local)
-        path = "C-ABI dcol_prox_batch_multi_gpu (pack_records + ncclAllGather, RCCL)"
+        try:
+            uid = [NativeComm.unique_id() if rank == 0 else None]
+            if dist is not None:
+                dist.broadcast_object_list(uid, src=0)
+            comm = NativeComm(uid[0], world, rank, local)
+        except Exception as e:   # recorded in the line; the step then uses torch.distributed
+            comm, native_error = None, f"{type(e).__name__}: {e}"
+        if dist is not None:     # every rank takes the same path
+            ok = torch.tensor([0.0 if comm is None else 1.0], device=coll_dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if ok.item() < 1.0 and comm is not None:
+                comm.close()
+                comm, native_error = None, native_error or "another rank could not create its communicator"
+        if comm is not None:
+            path = "C-ABI dcol_prox_batch_multi_gpu (pack_records + ncclAllGather, RCCL)"
     rec = torch.full((cap, REC), float("nan"), dtype=torch.float64, device=dev)
     gathered = torch.empty((world * cap, REC), dtype=torch.float64, device=dev if comm is not None else coll_dev)
 
@@ -576,6 +587,8 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
     }
     if comm is not None:
         line["rccl_world_size"] = world
+    if native_error:
+        line["native_comm_error"] = native_error
     if flops_local is not None:
         tf = flops_local / (solve_ms * 1e-3) / 1e12
         line["roofline_fp64"] = {"bound": "fp64-valu", "achieved": tf, "peak": FP64_VECTOR_PEAK_TFS,
