@@ -515,10 +515,37 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
     rec = torch.full((cap, REC), float("nan"), dtype=torch.float64, device=dev)
     gathered = torch.empty((world * cap, REC), dtype=torch.float64, device=dev if comm is not None else coll_dev)
 
+    lanes = []
     if comm is not None:
+        # steps issued round-robin on --streams HIP streams, each with its own communicator
+        # (collectives of one communicator are not issued from two streams) and buffers: the
+        # all-gather of one step overlaps the solve of the next (a batch service's steady
+        # state); the one-stream rate is reported beside it
+        comms = [comm]
+        for _ in range(max(1, args.streams) - 1):
+            try:
+                uid = [NativeComm.unique_id() if rank == 0 else None]
+                if dist is not None:
+                    dist.broadcast_object_list(uid, src=0)
+                comms.append(NativeComm(uid[0], world, rank, local))
+            except Exception as e:
+                native_error = f"extra stream communicator: {type(e).__name__}: {e}"
+                break
+        if dist is not None:     # every rank uses the same number of lanes
+            t = torch.tensor([float(len(comms))], device=coll_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            while len(comms) > int(t.item()):
+                comms.pop().close()
+        for j, c in enumerate(comms):
+            st = stream if j == 0 else torch.cuda.Stream(dev)
+            o = out if j == 0 else alloc_outputs(n, dev, want_grad=True, want_contact=False)
+            r_ = rec if j == 0 else torch.full((cap, REC), float("nan"), dtype=torch.float64, device=dev)
+            g_ = gathered if j == 0 else torch.empty((world * cap, REC), dtype=torch.float64, device=dev)
+            lanes.append(lambda c=c, st=st, o=o, r_=r_, g_=g_: c.solve_gather(
+                plan, d1, d2, cap, grad=args.grad, out=o, stream=st, rec_local=r_, rec_all=g_))
+
         def step():
-            comm.solve_gather(plan, d1, d2, cap, grad=args.grad, out=out, stream=stream, rec_local=rec,
-                              rec_all=gathered)
+            lanes[0]()
     else:
         def step():
             launch()
@@ -531,23 +558,28 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
             else:
                 gathered.copy_(rec)
 
-    for _ in range(warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], device=coll_dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t[0])
+    def timed(fns):
+        for k in range(warmup):
+            fns[k % len(fns)]()
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(steps):
+            fns[k % len(fns)]()
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([el], device=coll_dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t[0])
+        return el
+
+    elapsed_serial = timed([step]) if len(lanes) > 1 else None
+    elapsed = timed(lanes if len(lanes) > 1 else [step])
     # solve-only duration (HIP events on the launch stream; the plan's side-stream buckets
     # join back into it) -> FP64 roofline with the counted per-class flop model
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
@@ -564,9 +596,11 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
         solve_ms_max = float(t[0])
     else:
         solve_ms_max = solve_ms
+    torch.cuda.synchronize(dev)
     allrec = gathered.cpu().numpy().reshape(world, cap, REC)
     if comm is not None:
-        comm.close()
+        for c in comms:
+            c.close()
     if rank != 0:
         return None
     full = np.empty((B, REC))
@@ -584,6 +618,9 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
                    "parallelism": f"dp{world} (class-balanced shards)"},
         "solve_stats": {"ok_frac": float(np.mean(status == 0)), "iters_mean": float(full[status == 0, 14].mean())},
         "solve_ms_rank0": solve_ms, "solve_ms_max_rank": solve_ms_max,
+        "pipeline": {"streams": max(1, len(lanes)),
+                     "serial_value": B * steps / elapsed_serial if elapsed_serial else B * steps / elapsed,
+                     "serial_ms_per_step": 1e3 * (elapsed_serial or elapsed) / steps},
     }
     if comm is not None:
         line["rccl_world_size"] = world
