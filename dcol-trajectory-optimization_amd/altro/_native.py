@@ -53,6 +53,11 @@ SIGNATURES = {
                                        c_void_p, c_double, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_void_p]),
     "dcol_altro_victim_poses": (c_int, [POINTER(Model), c_int64, c_void_p, c_void_p]),
+    "dcol_altro_backward_pass": (c_int, [POINTER(Model), POINTER(Problem), c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_double, c_double,
+                                         c_void_p, c_void_p, POINTER(c_double), POINTER(c_double), POINTER(c_int64)]),
+    "dcol_altro_trial": (c_int, [POINTER(Model), c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_double, c_void_p,
+                                 c_void_p, c_void_p]),
     "dcol_altro_constraint_jacobian": (c_int, [POINTER(Model), c_int64, c_int32, c_void_p, c_void_p, c_void_p]),
 }
 
@@ -234,3 +239,35 @@ def constraint_jacobian(model: Model, X, dalpha):
     _check(load().dcol_altro_constraint_jacobian(ctypes.byref(model), N, D.shape[1], _ptr(X), _ptr(D), _ptr(G)),
            "dcol_altro_constraint_jacobian")
     return G
+
+
+def backward_pass(model: Model, prob: Problem, X, U, alpha, dalpha, A, B, mu, mux, lam, rho, reg):
+    """One backward pass in one call (dcol_altro_backward_pass): hx = 1 - alpha, constraint
+    Jacobian, stage terms, Riccati sweep and the AL cost of (X, U) -> (K, k, dJ, J).  Raises
+    numpy.linalg.LinAlgError when Quu is not positive definite (like backward())."""
+    N, nx, nu = prob.N, prob.nx, prob.nu
+    X, U, alpha, dalpha, A, B, mu, mux, lam = (_c(a) for a in (X, U, alpha, dalpha, A, B, mu, mux, lam))
+    K = np.empty((N - 1, nu, nx))
+    k = np.empty((N - 1, nu))
+    dJ, J, fail = c_double(), c_double(), c_int64(-1)
+    rc = load().dcol_altro_backward_pass(ctypes.byref(model), ctypes.byref(prob), _ptr(X), _ptr(U), _ptr(alpha),
+                                         _ptr(dalpha), _ptr(A), _ptr(B), _ptr(mu), _ptr(mux), _ptr(lam), float(rho),
+                                         float(reg), _ptr(K), _ptr(k), ctypes.byref(dJ), ctypes.byref(J),
+                                         ctypes.byref(fail))
+    if rc == ERR_NOT_PD:
+        raise np.linalg.LinAlgError(f"Quu is not positive definite at knot {fail.value}")
+    _check(rc, "dcol_altro_backward_pass")
+    return K, k, dJ.value, J.value
+
+
+def trial(model: Model, X, U, K, k, a):
+    """One line-search trial in one call (dcol_altro_trial): closed-loop rollout at step a
+    and the victim poses of the rolled-out states -> (Xn, Un, poses [T+1, 6])."""
+    X, U, K, k = _c(X), _c(U), _c(K), _c(k)
+    T = U.shape[0]
+    Xn = np.empty_like(X)
+    Un = np.empty_like(U)
+    P = np.empty((T + 1, 6))
+    _check(load().dcol_altro_trial(ctypes.byref(model), T, _ptr(X), _ptr(U), _ptr(K), _ptr(k), float(a), _ptr(Xn),
+                                   _ptr(Un), _ptr(P)), "dcol_altro_trial")
+    return Xn, Un, P

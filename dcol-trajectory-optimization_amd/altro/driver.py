@@ -189,11 +189,9 @@ def solve(params, X, U, prox=None, engine=None, verbose=True, prox_wide=None) ->
             at_x = (alpha, Jp, A, B)
         alpha, Jp, A, B = at_x
         hx = 1 - alpha
-        Gx = _native.constraint_jacobian(P.model, X, Jp)            # [N, ncx, nx]
-        lx, lu, lxx, luu, VxT, VxxT = _native.stage_terms(P.prob, X, U, hx, Gx, mu, mux, lam, rho)
-        K, k, dJ = _native.backward(A, B, lx, lu, lxx, luu, VxT, VxxT, reg)
+        # constraint Jacobian, stage terms, Riccati sweep and the cost of (X, U): one call
+        K, k, dJ, old = _native.backward_pass(P.model, P.prob, X, U, alpha, Jp, A, B, mu, mux, lam, rho, reg)
         # ---------------------------------------------------------------- forward pass
-        old = P.cost(X, U, hx, mu, mux, lam, rho)
         a, J, accepted = 1.0, old, False
         n_ls = int(params["max_linesearch_iters"])
         tried = 0
@@ -201,8 +199,8 @@ def solve(params, X, U, prox=None, engine=None, verbose=True, prox_wide=None) ->
             if tried == 0 or wide is None:
                 # the full step (accepted in most iterations), or every trial when no wide
                 # evaluator exists: one trajectory, Jacobians overlapped with its batch
-                Xn, Un = _native.rollout(P.model, X, U, K, k, a)
-                evaluate.submit(_native.victim_poses(P.model, Xn), True)
+                Xn, Un, poses = _native.trial(P.model, X, U, K, k, a)
+                evaluate.submit(poses, True)
                 An, Bn = _native.jacobians(P.model, Xn, Un)          # overlaps the GPU batch
                 an, Jn = evaluate.collect()
                 hxn = 1 - an

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <vector>
 
 namespace {
 
@@ -600,6 +601,44 @@ int dcol_altro_constraint_jacobian(const dcol_altro_model* m, int64_t N, int32_t
         }
     }
     return DCOL_ALTRO_OK;
+}
+
+// ---------------------------------------------------------------- fused driver steps
+// One call per optimizer phase instead of one per piece (the per-call cost of the Python
+// binding exceeded the work of the small pieces); each equals the calls it replaces.
+int dcol_altro_backward_pass(const dcol_altro_model* m, const dcol_altro_problem* p, const double* X,
+                             const double* U, const double* alpha, const double* dalpha, const double* A,
+                             const double* B, const double* mu, const double* mux, const double* lam, double rho,
+                             double reg, double* K, double* k, double* dJ, double* J, int64_t* fail_knot) {
+    if (!model_ok(m) || !problem_ok(p) || m->nx != p->nx || m->nu != p->nu || !X || !U || !A || !B || !K || !k ||
+        !dJ || !J || (p->ncx > 0 && (!alpha || !dalpha)))
+        return DCOL_ALTRO_ERR_ARG;
+    const int N = p->N, nx = p->nx, nu = p->nu, nc = p->ncx;
+    thread_local std::vector<double> ws;
+    const size_t need = (size_t)N * nc * (1 + nx) + (size_t)(N - 1) * (nx + nu + nx * nx + nu * nu) + nx + nx * nx;
+    if (ws.size() < need) ws.resize(need);
+    double* hx = ws.data();
+    double* Gx = hx + (size_t)N * nc;
+    double* lx = Gx + (size_t)N * nc * nx;
+    double* lu = lx + (size_t)(N - 1) * nx;
+    double* lxx = lu + (size_t)(N - 1) * nu;
+    double* luu = lxx + (size_t)(N - 1) * nx * nx;
+    double* VxT = luu + (size_t)(N - 1) * nu * nu;
+    double* VxxT = VxT + nx;
+    for (size_t i = 0; i < (size_t)N * nc; ++i) hx[i] = 1 - alpha[i];
+    int rc = dcol_altro_constraint_jacobian(m, N, nc, X, dalpha, Gx);
+    if (rc == DCOL_ALTRO_OK) rc = dcol_altro_stage_terms(p, X, U, hx, Gx, mu, mux, lam, rho, lx, lu, lxx, luu, VxT, VxxT);
+    if (rc == DCOL_ALTRO_OK)
+        rc = dcol_altro_backward(N - 1, nx, nu, A, B, lx, lu, lxx, luu, VxT, VxxT, reg, K, k, dJ, fail_knot);
+    if (rc == DCOL_ALTRO_OK) rc = dcol_altro_cost(p, X, U, hx, mu, mux, lam, rho, J);
+    return rc;
+}
+
+int dcol_altro_trial(const dcol_altro_model* m, int64_t T, const double* X, const double* U, const double* K,
+                     const double* k, double a, double* Xn, double* Un, double* poses) {
+    int rc = dcol_altro_rollout(m, T, X, U, K, k, a, Xn, Un);
+    if (rc == DCOL_ALTRO_OK) rc = dcol_altro_victim_poses(m, T + 1, Xn, poses);
+    return rc;
 }
 
 }  // extern "C"

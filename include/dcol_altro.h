@@ -119,6 +119,20 @@ int dcol_altro_stage_terms(const dcol_altro_problem* p, const double* X, const d
 /* Victim pose per knot, [N, 6] = (r, p MRP), from the state (system-specific map). */
 int dcol_altro_victim_poses(const dcol_altro_model* m, int64_t N, const double* X, double* poses);
 
+/* Fused driver phases (each equals the calls it replaces, in order):
+ * backward pass at (X, U) from the constraint batch (alpha [N, ncx], dalpha [N, ncx, 12])
+ * and the dynamics Jacobians A [N-1, nx, nx], B [N-1, nx, nu]: hx = 1 - alpha,
+ * dcol_altro_constraint_jacobian, dcol_altro_stage_terms, dcol_altro_backward (-> K, k,
+ * dJ, fail_knot) and dcol_altro_cost of (X, U) (-> J); */
+int dcol_altro_backward_pass(const dcol_altro_model* m, const dcol_altro_problem* p, const double* X,
+                             const double* U, const double* alpha, const double* dalpha, const double* A,
+                             const double* B, const double* mu, const double* mux, const double* lam, double rho,
+                             double reg, double* K, double* k, double* dJ, double* J, int64_t* fail_knot);
+/* one line-search trial: dcol_altro_rollout at step a, then dcol_altro_victim_poses of the
+ * T+1 rolled-out states -> poses [T+1, 6]. */
+int dcol_altro_trial(const dcol_altro_model* m, int64_t T, const double* X, const double* U, const double* K,
+                     const double* k, double a, double* Xn, double* Un, double* poses);
+
 /* d(1 - alpha)/dx [N, ncx, nx] from d alpha / d[r1, p1, r2, p2] [N, ncx, 12] (chain rule
  * through the pose map; the victim is primitive 1). */
 int dcol_altro_constraint_jacobian(const dcol_altro_model* m, int64_t N, int32_t ncx, const double* X,
