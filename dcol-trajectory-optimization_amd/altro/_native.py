@@ -13,7 +13,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("DCOL_ALTRO_LIB", os.path.join(PKG_ROOT, "lib", "libdcol_altro.so"))
 
 SYS_PIANO, SYS_QUADROTOR, SYS_RIGID = 0, 1, 2
-OK, ERR_ARG, ERR_NOT_PD = 0, -1, -2
+OK, ERR_ARG, ERR_NOT_PD, ERR_DEVICE = 0, -1, -2, -3
 ABI_VERSION = 1
 MAX_NX, MAX_NU = 16, 8
 

@@ -10,9 +10,11 @@ reference optimizer (ALTRO.py:365-488); what changes is how the work is issued:
     (ALTRO.py:268-300) and compute_jacobian         ONE batch of N x n_obs pairs WITH
     per knot (ALTRO.py:77-100)                      gradients on the GPU, and the dynamics
                                                     Jacobians of its trajectory were computed
-                                                    on the host (dcol_altro_jacobians, all
-                                                    knots) while that batch ran; only the
-                                                    first iteration launches its own batch
+                                                    in the same submission, all knots in one
+                                                    launch behind the solves (jacobians.py;
+                                                    host fallback: dcol_altro_jacobians);
+                                                    only the first iteration launches its
+                                                    own batch
   Riccati loop with scipy cho_factor (:304-336)    dcol_altro_backward, native
   forward_pass: old cost recomputed per line-      old cost from the cached alpha; per trial
     search trial, rollout + N x n_obs solves        one native rollout + ONE batch (alpha and
@@ -29,11 +31,13 @@ from __future__ import annotations
 
 import dataclasses
 import logging
+import os
 import time
 
 import numpy as np
 
 from . import _native
+from . import jacobians as _jacobians
 from . import systems as _systems
 
 log = logging.getLogger("altro")
@@ -59,6 +63,7 @@ class AltroResult:
     prox_s: float = 0.0                # time inside proximity batches (H2D + kernel + D2H)
     prox_batches: int = 0
     prox_pairs: int = 0
+    jacobians: str = "host"            # where the dynamics Jacobians ran ("device" / "host")
 
     @property
     def ms_per_iter(self) -> float:
@@ -156,6 +161,9 @@ def solve(params, X, U, prox=None, engine=None, verbose=True, prox_wide=None) ->
         # after a rejected full step, TRIALS step lengths per batch
         wide = _Timed(ObstacleField(params["P_vic"], params["P_obs"], TRIALS * N, engine=engine))
     evaluate = _Timed(prox)
+    # dynamics Jacobians: on the constraint batch's stream when it has one (GPU), else host
+    jac = _jacobians.provider(P.model, N - 1, getattr(prox, "stream", None),
+                              os.environ.get("DCOL_ALTRO_JAC", "device"))
     t_start = time.perf_counter()          # one-time set-up (shape table, plan, warm-up) excluded
     ncx = P.ncx
     if int(params.get("ncx", ncx)) != ncx or int(params.get("ncu", 2 * nu)) != 2 * nu:
@@ -169,7 +177,7 @@ def solve(params, X, U, prox=None, engine=None, verbose=True, prox_wide=None) ->
     mu = np.zeros((N - 1, 2 * nu))
     mux = np.zeros((N, ncx))
     lam = np.zeros(nx)
-    res = AltroResult(X=X, U=U, converged=False, iterations=0)
+    res = AltroResult(X=X, U=U, converged=False, iterations=0, jacobians=jac.where)
     hx_cur = None            # 1 - alpha at the current X, when known from the last accepted trial
     # (alpha, d alpha, A, B) at the current (X, U): every line-search trial is solved WITH
     # gradients and its dynamics Jacobians are computed on the host while the GPU batch runs,
@@ -184,9 +192,9 @@ def solve(params, X, U, prox=None, engine=None, verbose=True, prox_wide=None) ->
         # ---------------------------------------------------------------- backward pass
         if at_x is None:
             evaluate.submit(_native.victim_poses(P.model, X), True)
-            A, B = _native.jacobians(P.model, X, U)                  # overlaps the GPU batch
+            jac.submit(X, U)                                         # behind / beside the batch
             alpha, Jp = evaluate.collect()
-            at_x = (alpha, Jp, A, B)
+            at_x = (alpha, Jp) + jac.collect()
         alpha, Jp, A, B = at_x
         hx = 1 - alpha
         # constraint Jacobian, stage terms, Riccati sweep and the cost of (X, U): one call
@@ -201,8 +209,9 @@ def solve(params, X, U, prox=None, engine=None, verbose=True, prox_wide=None) ->
                 # evaluator exists: one trajectory, Jacobians overlapped with its batch
                 Xn, Un, poses = _native.trial(P.model, X, U, K, k, a)
                 evaluate.submit(poses, True)
-                An, Bn = _native.jacobians(P.model, Xn, Un)          # overlaps the GPU batch
+                jac.submit(Xn, Un)                                   # behind / beside the batch
                 an, Jn = evaluate.collect()
+                An, Bn = jac.collect()
                 hxn = 1 - an
                 new = P.cost(Xn, Un, hxn, mu, mux, lam, rho)
                 tried += 1
@@ -228,8 +237,8 @@ def solve(params, X, U, prox=None, engine=None, verbose=True, prox_wide=None) ->
                 tried += 1
                 if new < old:
                     X, U, J, accepted, hx_cur = Xs[j], Us[j], new, True, hxn
-                    A_, B_ = _native.jacobians(P.model, X, U)
-                    at_x = (ans[j].copy(), Jns[j].copy(), A_, B_)
+                    jac.submit(X, U)
+                    at_x = (ans[j].copy(), Jns[j].copy()) + jac.collect()
                     break
                 a *= 0.5
         if not accepted:

@@ -259,10 +259,11 @@ bool cone_disabled() {
 // buckets up to twice its rows (a tight bucket compiled only with LPP 2 -- 6 or 10 rows --
 // loses to the next bucket's 8-lane groups), fewer rows on ties.
 void latency_config(Launch& L) {
-    int best_o = L.omax, best_l = max_lpp(L.N, L.nsoc, L.omax);
+    const int fl = L.ball ? 2 : (L.cone ? 4 : 0);
+    int best_o = L.omax, best_l = max_lpp(L.N, L.nsoc, L.omax, fl);
     for (const int om : buckets().at({L.N, L.nsoc})) {
         if (om <= L.omax || om > 2 * L.omax) continue;
-        const int l = max_lpp(L.N, L.nsoc, om);
+        const int l = max_lpp(L.N, L.nsoc, om, fl);
         if (om * best_l < best_o * l) {   // om / l < best_o / best_l
             best_o = om;
             best_l = l;
@@ -301,6 +302,7 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
         const int ball = c.nsoc == 0 ? 0
                          : (none_cone && !ball_disabled()) ? 1
                          : (all_cone && c.N == 4 && !cone_disabled()) ? 2 : 0;
+        if (c.status == DCOL_OK && ball) c.lpp = choose_lpp(c.N, c.nsoc, c.omax, 2 * ball);   // flavour's own list
         Key k = c.status == DCOL_OK ? Key{0, c.N, c.nsoc, c.omax, c.lpp, ball, 0} : Key{1, 0, 0, 0, 0, 0, c.status};
         auto it = gid_of_key.emplace(k, (int32_t)groups.size()).first;
         if (it->second == (int32_t)groups.size()) groups.push_back(Group{k});

@@ -39,20 +39,34 @@ inline const std::map<std::pair<int, int>, std::vector<int>>& buckets() {
     return m;
 }
 
-// lanes per pair for a kernel shape: the first compiled LPP, or DCOL_LPP=<n> if that
-// alternative is compiled for the shape (A/B experiments)
+// Compiled (LPP, WPS) list of a kernel shape in one flavour: fl 2 the ball-SOC copies, 4 the
+// structured-cone copies, else the dense kernels (variants.py CONFIG / CONFIG_FL); the
+// first entry is the throughput choice.
+#define DCOL_FOR_FLAVOUR(fl, X)          \
+    do {                                 \
+        if ((fl) == 2) {                 \
+            DCOL_BALL_VARIANTS(X)        \
+        } else if ((fl) == 4) {          \
+            DCOL_CONE_VARIANTS(X)        \
+        } else {                         \
+            DCOL_VARIANTS(X)             \
+        }                                \
+    } while (0)
+
 // largest compiled LPP for a kernel shape (latency choice for launches that leave the GPU
 // mostly idle)
-inline int max_lpp(int N, int nsoc, int omax) {
+inline int max_lpp(int N, int nsoc, int omax, int fl = 0) {
     int best = 0;
 #define DCOL_MAXL(NN, NS, OM, LP, WP, FL) \
     if (NN == N && NS == nsoc && OM == omax && LP > best) best = LP;
-    DCOL_VARIANTS(DCOL_MAXL)
+    DCOL_FOR_FLAVOUR(fl, DCOL_MAXL);
 #undef DCOL_MAXL
     return best;
 }
 inline bool lpp_forced() { return std::getenv("DCOL_LPP") != nullptr; }
-inline int choose_lpp(int N, int nsoc, int omax) {
+// lanes per pair for a kernel shape: the first compiled LPP of the flavour, or DCOL_LPP=<n>
+// if that alternative is compiled (A/B experiments)
+inline int choose_lpp(int N, int nsoc, int omax, int fl = 0) {
     static const int forced = [] {
         const char* e = std::getenv("DCOL_LPP");
         return e ? std::atoi(e) : 0;
@@ -63,7 +77,7 @@ inline int choose_lpp(int N, int nsoc, int omax) {
         if (first == 0) first = LP;                                \
         if (forced == LP) return LP;                               \
     }
-    DCOL_VARIANTS(DCOL_PICK)
+    DCOL_FOR_FLAVOUR(fl, DCOL_PICK);
 #undef DCOL_PICK
     return first;
 }

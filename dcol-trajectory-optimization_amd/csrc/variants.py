@@ -85,6 +85,9 @@ CONFIG = {
     (6, 2, 4): [(2, 1), (4, 1)],
     (6, 2, 8): [(2, 1), (8, 1)],
 }
+# per-flavour overrides for the structured copies (FL 2 = BALL, 4 = CONE): their register
+# footprint differs from the dense kernel's, so their spill-free (LPP, WPS) can too
+CONFIG_FL = {}
 FULL = {(4, 0)}   # shapes with padding-free copies (see module docstring)
 
 
@@ -125,6 +128,11 @@ def configs(n, nsoc, omax):
     return [(4, 1)] if omax % 4 == 0 else [(2, 1)]
 
 
+def configs_fl(n, nsoc, omax, fl):
+    """(LPP, WPS) list of one flavour's copies (fl 0 dense, 1 FULL, 2 BALL, 4 CONE)"""
+    return CONFIG_FL.get((n, nsoc, omax, fl), configs(n, nsoc, omax))
+
+
 def fused():
     out = []
     for (n, s), os_ in sorted(OMAX.items()):
@@ -137,10 +145,11 @@ def fused():
             out.append((n, s, o, lpp, 0))
             if (n, s) in FULL:
                 out.append((n, s, o, lpp, 1))
-            if ball(n, s) and (n, s, o, lpp) not in BALL_SKIP:
-                out.append((n, s, o, lpp, 2))
+            lb = max(l for l, _ in configs_fl(n, s, o, 2))
+            if ball(n, s) and (n, s, o, lb) not in BALL_SKIP:
+                out.append((n, s, o, lb, 2))
             if cone(n, s, o):
-                out.append((n, s, o, lpp, 4))
+                out.append((n, s, o, max(l for l, _ in configs_fl(n, s, o, 4)), 4))
     return out
 
 
@@ -152,10 +161,11 @@ def main():
     lines += ["", "#define DCOL_FULL_VARIANTS(X) \\"]
     lines += [f"    X({n}, {s}, {o}, {l}, {w}, 1) \\" for n, s, o in shapes if (n, s) in FULL for l, w in configs(n, s, o)]
     lines += ["", "#define DCOL_BALL_VARIANTS(X) \\"]
-    lines += [f"    X({n}, {s}, {o}, {l}, {w}, 2) \\" for n, s, o in shapes if ball(n, s) for l, w in configs(n, s, o)
-              if (n, s, o, l) not in BALL_SKIP]
+    lines += [f"    X({n}, {s}, {o}, {l}, {w}, 2) \\" for n, s, o in shapes if ball(n, s)
+              for l, w in configs_fl(n, s, o, 2) if (n, s, o, l) not in BALL_SKIP]
     lines += ["", "#define DCOL_CONE_VARIANTS(X) \\"]
-    lines += [f"    X({n}, {s}, {o}, {l}, {w}, 4) \\" for n, s, o in shapes if cone(n, s, o) for l, w in configs(n, s, o)]
+    lines += [f"    X({n}, {s}, {o}, {l}, {w}, 4) \\" for n, s, o in shapes if cone(n, s, o)
+              for l, w in configs_fl(n, s, o, 4)]
     lines += ["", "#define DCOL_SHAPES(X) \\"]
     lines += [f"    X({n}, {s}, {o}) \\" for n, s, o in shapes]
     lines += ["", "#define DCOL_FUSED_VARIANTS(X) \\"]

@@ -10,7 +10,8 @@
  *     piano_mover.py:7-47, cluttered_hallway_quadrotor.py:      (batched over states)
  *     19-105, cone_through_wall.py:19-86
  *   ALTRO.py compute_jacobian (forward differences,           dcol_altro_jacobians()
- *     delta 1e-6) called per knot at ALTRO.py:289-290           (all knots in one call)
+ *     delta 1e-6) called per knot at ALTRO.py:289-290           (all knots in one call),
+ *                                                               (GPU: dcol_altro_device.h)
  *   ALTRO.py backward_pass Riccati recursion :304-336          dcol_altro_backward()
  *     (Quu = luu + B'(Vxx+reg I)B, scipy cho_factor/solve)
  *   ALTRO.py forward_pass rollout :214-217                     dcol_altro_rollout(), dcol_altro_rollouts()
@@ -45,7 +46,8 @@ enum dcol_altro_system {
 enum dcol_altro_error {
     DCOL_ALTRO_OK = 0,
     DCOL_ALTRO_ERR_ARG = -1,    /* bad pointer / size / system id                             */
-    DCOL_ALTRO_ERR_NOT_PD = -2  /* Quu not positive definite (scipy cho_factor LinAlgError)    */
+    DCOL_ALTRO_ERR_NOT_PD = -2, /* Quu not positive definite (scipy cho_factor LinAlgError)    */
+    DCOL_ALTRO_ERR_DEVICE = -3  /* kernel launch failed (device entry point)                  */
 };
 
 /* Physical constants of a model.  Fields a system does not use are ignored. */

@@ -232,6 +232,7 @@ def test_altro_run_matches_reference_gpu(name):
     g = np.load(os.path.join(GOLDEN, "altro", f"altro_{name}.npz"))
     params, X, U = systems.initialize(name)
     r = solve(params, X, U, verbose=False)
+    assert r.jacobians == "device"   # dynamics Jacobians batched over knots on the GPU (section 8 f3)
     check_run(r, g)
     # one batch for the first backward pass, then per iteration one for the full step and one
     # per TRIALS retries after it: every accepted trial's batch (with gradients) serves the

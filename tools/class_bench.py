@@ -7,7 +7,7 @@ For every ordered kind pair of the mixed workload (27 supported ones), B pairs o
 class are solved with FD gradients; prints per class the variant launched, pair-solves/s,
 kernel ms and mean / max Newton iterations.  Also times a latency-size batch (default 1,000
 pairs) per class.
-Usage: python3 tools/class_bench.py [--pairs 200000] [--small 1000] [--reps 10]
+Usage: python3 tools/class_bench.py [--pairs 200000] [--small 1000 (0: skip)] [--reps 10] [--classes a-b,...]
 """
 import argparse
 import json
@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--pairs", type=int, default=200_000)
     ap.add_argument("--small", type=int, default=1000)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--classes", default="", help="comma-separated class names (default: all 27)")
     args = ap.parse_args()
     import torch
     from dcol_amd import Engine, alloc_outputs, spec_from_arrays
@@ -43,9 +44,14 @@ def main():
     rng = np.random.default_rng(0)
     stream = torch.cuda.current_stream(dev)
     rows = []
+    if args.classes:
+        want = set(args.classes.split(","))
+        combos = [(a, b) for a, b in combos if f"{NAMES[a]}-{NAMES[b]}" in want]
     for a, b in combos:
         rec = {"class": f"{NAMES[a]}-{NAMES[b]}"}
         for label, B in (("big", args.pairs), ("small", args.small)):
+            if B <= 0:
+                continue
             s1 = rng.choice(by_kind[a], B).astype(np.int32)
             s2 = rng.choice(by_kind[b], B).astype(np.int32)
             p1 = np.hstack([rng.uniform(-3, 3, (B, 3)), rng.uniform(-1, 1, (B, 3))])
