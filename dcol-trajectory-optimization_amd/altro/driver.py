@@ -11,7 +11,7 @@ reference optimizer (ALTRO.py:365-488); what changes is how the work is issued:
     per knot (ALTRO.py:77-100)                      gradients on the GPU, and the dynamics
                                                     Jacobians of its trajectory were computed
                                                     in the same submission, all knots in one
-                                                    launch behind the solves (jacobians.py;
+                                                    launch beside the solves (jacobians.py;
                                                     host fallback: dcol_altro_jacobians);
                                                     only the first iteration launches its
                                                     own batch
@@ -161,8 +161,9 @@ def solve(params, X, U, prox=None, engine=None, verbose=True, prox_wide=None) ->
         # after a rejected full step, TRIALS step lengths per batch
         wide = _Timed(ObstacleField(params["P_vic"], params["P_obs"], TRIALS * N, engine=engine))
     evaluate = _Timed(prox)
-    # dynamics Jacobians: on the constraint batch's stream when it has one (GPU), else host
-    jac = _jacobians.provider(P.model, N - 1, getattr(prox, "stream", None),
+    # dynamics Jacobians: on the GPU beside the constraint batches when those run there
+    stream = getattr(prox, "stream", None)
+    jac = _jacobians.provider(P.model, N - 1, stream.device.index if stream is not None else None,
                               os.environ.get("DCOL_ALTRO_JAC", "device"))
     t_start = time.perf_counter()          # one-time set-up (shape table, plan, warm-up) excluded
     ncx = P.ncx
@@ -192,7 +193,7 @@ def solve(params, X, U, prox=None, engine=None, verbose=True, prox_wide=None) ->
         # ---------------------------------------------------------------- backward pass
         if at_x is None:
             evaluate.submit(_native.victim_poses(P.model, X), True)
-            jac.submit(X, U)                                         # behind / beside the batch
+            jac.submit(X, U)                                         # beside the batch
             alpha, Jp = evaluate.collect()
             at_x = (alpha, Jp) + jac.collect()
         alpha, Jp, A, B = at_x
@@ -209,7 +210,7 @@ def solve(params, X, U, prox=None, engine=None, verbose=True, prox_wide=None) ->
                 # evaluator exists: one trajectory, Jacobians overlapped with its batch
                 Xn, Un, poses = _native.trial(P.model, X, U, K, k, a)
                 evaluate.submit(poses, True)
-                jac.submit(Xn, Un)                                   # behind / beside the batch
+                jac.submit(Xn, Un)                                   # beside the batch
                 an, Jn = evaluate.collect()
                 An, Bn = jac.collect()
                 hxn = 1 - an

@@ -4,13 +4,14 @@ The reference differentiates the discrete dynamics knot by knot (compute_jacobia
 ALTRO.py:77-100, per knot at :289-290).  Here every knot of a trajectory goes in one call:
 
   DeviceJacobians  one GPU launch over all knots (dcol_altro_jacobians_device in libdcol.so,
-                   include/dcol_altro_device.h), queued on the
-                   constraint batch's stream right behind its proximity solves, reading the
-                   trajectory from and writing A, B to device-mapped pinned host buffers;
+                   include/dcol_altro_device.h) on a stream of its
+                   own, so it runs beside the constraint batch's proximity solves (a phase
+                   fills a few CUs), reading the trajectory from and writing A, B to
+                   device-mapped pinned host buffers;
   HostJacobians    the host library's dcol_altro_jacobians (OpenMP over knots).
 
 Both give bitwise the same A, B (tests/test_altro_device.py).  The driver picks the device
-path when the constraint evaluator runs on a HIP stream (DCOL_ALTRO_JAC=host forces the host
+path when the constraint evaluator runs on the GPU (DCOL_ALTRO_JAC=host forces the host
 one).  submit() starts the work, collect() returns (A [T, nx, nx], B [T, nx, nu]).
 """
 from __future__ import annotations
@@ -53,13 +54,15 @@ def _device_fn():
 
 
 class DeviceJacobians:
-    """Jacobians of trajectories of T + 1 states on the GPU, on `stream` (a torch stream)."""
+    """Jacobians of trajectories of T + 1 states on the GPU, on a stream of their own on
+    `device` (index)."""
     where = "device"
 
-    def __init__(self, model, T, stream):
+    def __init__(self, model, T, device):
         import torch
         from dcol_amd import _lib
-        self.model, self.T, self.stream = model, int(T), stream
+        self.model, self.T = model, int(T)
+        self.stream = stream = torch.cuda.Stream(torch.device("cuda", int(device)))
         nx, nu = model.nx, model.nu
         n = self.T * (nx + nu + nx * nx + nx * nu)
         self._buf = torch.empty(max(n, 1), dtype=torch.float64, pin_memory=True)
@@ -77,6 +80,8 @@ class DeviceJacobians:
                       c_void_p(stream.cuda_stream))
         self._fn = _device_fn()
         self._pending = False
+        self.submit(np.zeros((self.T, nx)), np.zeros((self.T, nu)))   # load the code object now
+        self.collect()
 
     def submit(self, X, U):
         self._x[:] = np.asarray(X, dtype=np.float64).reshape(-1, self.model.nx)[: self.T]
@@ -92,12 +97,12 @@ class DeviceJacobians:
         return self._a.copy(), self._b.copy()
 
 
-def provider(model, T, stream=None, mode="device"):
-    """DeviceJacobians on `stream` when mode == "device" and the GPU path is available, else
-    HostJacobians."""
-    if mode == "device" and stream is not None:
+def provider(model, T, device=None, mode="device"):
+    """DeviceJacobians on GPU `device` when mode == "device" and the GPU path is available,
+    else HostJacobians."""
+    if mode == "device" and device is not None:
         try:
-            return DeviceJacobians(model, T, stream)
+            return DeviceJacobians(model, T, device)
         except DeviceUnavailable:
             pass
     return HostJacobians(model)
