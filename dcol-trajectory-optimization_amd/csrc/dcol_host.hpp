@@ -61,7 +61,7 @@ inline int max_lpp(int N, int nsoc, int omax, int fl = 0) {
     if (NN == N && NS == nsoc && OM == omax && LP > best) best = LP;
     DCOL_FOR_FLAVOUR(fl, DCOL_MAXL);
 #undef DCOL_MAXL
-    return best;
+    return (best == 0 && fl != 0) ? max_lpp(N, nsoc, omax, 0) : best;   // no copies of the flavour: dense
 }
 inline bool lpp_forced() { return std::getenv("DCOL_LPP") != nullptr; }
 // lanes per pair for a kernel shape: the first compiled LPP of the flavour, or DCOL_LPP=<n>
@@ -79,7 +79,7 @@ inline int choose_lpp(int N, int nsoc, int omax, int fl = 0) {
     }
     DCOL_FOR_FLAVOUR(fl, DCOL_PICK);
 #undef DCOL_PICK
-    return first;
+    return (first == 0 && fl != 0) ? choose_lpp(N, nsoc, omax, 0) : first;   // no copies of the flavour: dense
 }
 
 // Static digest of one primitive (misc_primitive_constructor.py:4-88 ->
