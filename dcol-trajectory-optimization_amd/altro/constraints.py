@@ -162,9 +162,12 @@ class ObstacleField:
                 self.h_out[:n].copy_(self.d_out[:n], non_blocking=True)
         self._pending = bool(grad)
 
-    def collect(self):
+    soa_grad = True   # collect(soa=True): gradients in the engine's [12, N n_obs] layout
+
+    def collect(self, soa=False):
         """Wait for the phase started by submit() -> (alpha [N, n_obs], J [N, n_obs, 12] |
-        None).  Raises like the reference on the first failed pair (knot-major order)."""
+        None), or J [12, N n_obs] with soa=True (no transpose).  Raises like the reference on
+        the first failed pair (knot-major order)."""
         grad = self._pending
         self._pending = None
         if grad is None:
@@ -176,7 +179,10 @@ class ObstacleField:
         if st.any():
             raise_for_status(int(st[np.flatnonzero(st)[0]]))
         alpha = self._np_alpha.reshape(self.N, self.n_obs).copy()
-        J = self._np_grad.T.reshape(self.N, self.n_obs, 12).copy() if grad else None
+        if not grad:
+            J = None
+        else:
+            J = self._np_grad.copy() if soa else self._np_grad.T.reshape(self.N, self.n_obs, 12).copy()
         return alpha, J
 
     def evaluate(self, victim_poses, grad: bool):

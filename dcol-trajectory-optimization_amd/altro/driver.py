@@ -90,11 +90,19 @@ class _Timed:
         self._job = (poses, grad)
         self.seconds += time.perf_counter() - t0
 
+    @property
+    def soa(self):
+        """the evaluator returns gradients in the engine's component-major layout on request"""
+        return self.async_ and getattr(self.field, "soa_grad", False)
+
     def collect(self):
         t0 = time.perf_counter()
         poses, grad = self._job
         self._job = None
-        out = self.field.collect() if self.async_ else self.field.evaluate(poses, grad)
+        if self.soa:
+            out = self.field.collect(soa=True)
+        else:
+            out = self.field.collect() if self.async_ else self.field.evaluate(poses, grad)
         self.seconds += time.perf_counter() - t0
         self.batches += 1
         self.pairs += poses.shape[0] * out[0].shape[1]
@@ -199,7 +207,9 @@ def solve(params, X, U, prox=None, engine=None, verbose=True, prox_wide=None) ->
         alpha, Jp, A, B = at_x
         hx = 1 - alpha
         # constraint Jacobian, stage terms, Riccati sweep and the cost of (X, U): one call
-        K, k, dJ, old = _native.backward_pass(P.model, P.prob, X, U, alpha, Jp, A, B, mu, mux, lam, rho, reg)
+        # (gradients in the engine's [12, N ncx] layout when they came from the GPU batch)
+        K, k, dJ, old = _native.backward_pass(P.model, P.prob, X, U, alpha, Jp, A, B, mu, mux, lam, rho, reg,
+                                              soa=Jp.ndim == 2)
         # ---------------------------------------------------------------- forward pass
         a, J, accepted = 1.0, old, False
         n_ls = int(params["max_linesearch_iters"])
@@ -231,7 +241,8 @@ def solve(params, X, U, prox=None, engine=None, verbose=True, prox_wide=None) ->
             wide.submit(_native.victim_poses(P.model, Xs.reshape(-1, nx)), True)
             ans, Jns = wide.collect()
             ans = ans.reshape(TRIALS, N, ncx)
-            Jns = Jns.reshape(TRIALS, N, ncx, 12)
+            if not wide.soa:
+                Jns = Jns.reshape(TRIALS, N, ncx, 12)
             for j in range(w):
                 hxn = 1 - ans[j]
                 new = P.cost(Xs[j], Us[j], hxn, mu, mux, lam, rho)
@@ -239,7 +250,8 @@ def solve(params, X, U, prox=None, engine=None, verbose=True, prox_wide=None) ->
                 if new < old:
                     X, U, J, accepted, hx_cur = Xs[j], Us[j], new, True, hxn
                     jac.submit(X, U)
-                    at_x = (ans[j].copy(), Jns[j].copy()) + jac.collect()
+                    Jj = Jns[:, j * N * ncx:(j + 1) * N * ncx] if wide.soa else Jns[j]
+                    at_x = (ans[j].copy(), Jj.copy()) + jac.collect()
                     break
                 a *= 0.5
         if not accepted:

@@ -397,9 +397,10 @@ int dcol_altro_victim_poses(const dcol_altro_model* m, int64_t N, const double* 
     return DCOL_ALTRO_OK;
 }
 
-int dcol_altro_constraint_jacobian(const dcol_altro_model* m, int64_t N, int32_t ncx, const double* X,
-                                   const double* dalpha, double* Gx) {
-    if (!model_ok(m) || N < 0 || ncx < 0 || (N > 0 && ncx > 0 && (!X || !dalpha || !Gx))) return DCOL_ALTRO_ERR_ARG;
+namespace {
+// element (pair i = t ncx + k, component c) of dalpha at dalpha[i s_pair + c s_comp]
+int constraint_jacobian_strided(const dcol_altro_model* m, int64_t N, int32_t ncx, const double* X,
+                                const double* dalpha, int64_t s_pair, int64_t s_comp, double* Gx) {
     const int nx = m->nx;
     for (int64_t t = 0; t < N; ++t) {
         const double* x = X + t * nx;
@@ -409,7 +410,9 @@ int dcol_altro_constraint_jacobian(const dcol_altro_model* m, int64_t N, int32_t
             c = 1 / (4 * (cs * cs));
         }
         for (int k = 0; k < ncx; ++k) {
-            const double* J = dalpha + (t * ncx + k) * 12;
+            const double* Jp = dalpha + (t * ncx + k) * s_pair;
+            double J[6];   // d alpha / d (r1, p1): the victim's pose
+            for (int i = 0; i < 6; ++i) J[i] = Jp[i * s_comp];
             double* g = Gx + (t * ncx + k) * nx;
             for (int i = 0; i < nx; ++i) g[i] = 0.0;
             if (m->system == DCOL_SYS_PIANO) {
@@ -426,16 +429,23 @@ int dcol_altro_constraint_jacobian(const dcol_altro_model* m, int64_t N, int32_t
     }
     return DCOL_ALTRO_OK;
 }
+}  // namespace
+
+extern "C" int dcol_altro_constraint_jacobian(const dcol_altro_model* m, int64_t N, int32_t ncx, const double* X,
+                                              const double* dalpha, double* Gx) {
+    if (!model_ok(m) || N < 0 || ncx < 0 || (N > 0 && ncx > 0 && (!X || !dalpha || !Gx))) return DCOL_ALTRO_ERR_ARG;
+    return constraint_jacobian_strided(m, N, ncx, X, dalpha, 12, 1, Gx);
+}
 
 // ---------------------------------------------------------------- fused driver steps
 // One call per optimizer phase instead of one per piece (the per-call cost of the Python
 // binding exceeded the work of the small pieces); each equals the calls it replaces.
 int dcol_altro_backward_pass(const dcol_altro_model* m, const dcol_altro_problem* p, const double* X,
-                             const double* U, const double* alpha, const double* dalpha, const double* A,
-                             const double* B, const double* mu, const double* mux, const double* lam, double rho,
-                             double reg, double* K, double* k, double* dJ, double* J, int64_t* fail_knot) {
+                             const double* U, const double* alpha, const double* dalpha, int64_t dalpha_comp_stride,
+                             const double* A, const double* B, const double* mu, const double* mux, const double* lam,
+                             double rho, double reg, double* K, double* k, double* dJ, double* J, int64_t* fail_knot) {
     if (!model_ok(m) || !problem_ok(p) || m->nx != p->nx || m->nu != p->nu || !X || !U || !A || !B || !K || !k ||
-        !dJ || !J || (p->ncx > 0 && (!alpha || !dalpha)))
+        !dJ || !J || (p->ncx > 0 && (!alpha || !dalpha)) || dalpha_comp_stride < 0)
         return DCOL_ALTRO_ERR_ARG;
     const int N = p->N, nx = p->nx, nu = p->nu, nc = p->ncx;
     thread_local std::vector<double> ws;
@@ -450,7 +460,8 @@ int dcol_altro_backward_pass(const dcol_altro_model* m, const dcol_altro_problem
     double* VxT = luu + (size_t)(N - 1) * nu * nu;
     double* VxxT = VxT + nx;
     for (size_t i = 0; i < (size_t)N * nc; ++i) hx[i] = 1 - alpha[i];
-    int rc = dcol_altro_constraint_jacobian(m, N, nc, X, dalpha, Gx);
+    int rc = dalpha_comp_stride ? constraint_jacobian_strided(m, N, nc, X, dalpha, 1, dalpha_comp_stride, Gx)
+                                : constraint_jacobian_strided(m, N, nc, X, dalpha, 12, 1, Gx);
     if (rc == DCOL_ALTRO_OK) rc = dcol_altro_stage_terms(p, X, U, hx, Gx, mu, mux, lam, rho, lx, lu, lxx, luu, VxT, VxxT);
     if (rc == DCOL_ALTRO_OK)
         rc = dcol_altro_backward(N - 1, nx, nu, A, B, lx, lu, lxx, luu, VxT, VxxT, reg, K, k, dJ, fail_knot);

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define DCOL_ALTRO_ABI_VERSION 1
+#define DCOL_ALTRO_ABI_VERSION 2
 #define DCOL_ALTRO_MAX_NX 16
 #define DCOL_ALTRO_MAX_NU 8
 
@@ -122,14 +122,16 @@ int dcol_altro_stage_terms(const dcol_altro_problem* p, const double* X, const d
 int dcol_altro_victim_poses(const dcol_altro_model* m, int64_t N, const double* X, double* poses);
 
 /* Fused driver phases (each equals the calls it replaces, in order):
- * backward pass at (X, U) from the constraint batch (alpha [N, ncx], dalpha [N, ncx, 12])
+ * backward pass at (X, U) from the constraint batch (alpha [N, ncx]; dalpha [N, ncx, 12] when
+ * dalpha_comp_stride is 0, else the engine's component-major layout: component c of pair i
+ * at dalpha[c * dalpha_comp_stride + i], e.g. dcol_plan_run's grad[12][B] as it comes back)
  * and the dynamics Jacobians A [N-1, nx, nx], B [N-1, nx, nu]: hx = 1 - alpha,
  * dcol_altro_constraint_jacobian, dcol_altro_stage_terms, dcol_altro_backward (-> K, k,
  * dJ, fail_knot) and dcol_altro_cost of (X, U) (-> J); */
 int dcol_altro_backward_pass(const dcol_altro_model* m, const dcol_altro_problem* p, const double* X,
-                             const double* U, const double* alpha, const double* dalpha, const double* A,
-                             const double* B, const double* mu, const double* mux, const double* lam, double rho,
-                             double reg, double* K, double* k, double* dJ, double* J, int64_t* fail_knot);
+                             const double* U, const double* alpha, const double* dalpha, int64_t dalpha_comp_stride,
+                             const double* A, const double* B, const double* mu, const double* mux, const double* lam,
+                             double rho, double reg, double* K, double* k, double* dJ, double* J, int64_t* fail_knot);
 /* one line-search trial: dcol_altro_rollout at step a, then dcol_altro_victim_poses of the
  * T+1 rolled-out states -> poses [T+1, 6]. */
 int dcol_altro_trial(const dcol_altro_model* m, int64_t T, const double* X, const double* U, const double* K,

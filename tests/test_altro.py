@@ -331,6 +331,31 @@ def test_al_cost_and_stage_terms_match_reference_math(name):
             np.testing.assert_allclose(a, b, rtol=1e-12, atol=1e-12 * max(1.0, np.abs(b).max()))
 
 
+def test_backward_pass_component_major_gradients_equal():
+    """dcol_altro_backward_pass on the engine's [12, N ncx] gradient layout (what the GPU
+    batch returns) equals the call on [N, ncx, 12]: same K, k, dJ, J bitwise."""
+    from altro import _native as nat
+    from altro import systems
+    from altro.driver import _Problem
+    params, X, U = systems.initialize("quadrotor")
+    P = _Problem(params)
+    N, nx, nu, ncx = P.N, P.nx, P.nu, P.ncx
+    rng = np.random.default_rng(11)
+    X = np.asarray(X, dtype=np.float64).reshape(N, nx) + 0.01 * rng.normal(size=(N, nx))
+    U = np.asarray(U, dtype=np.float64).reshape(N - 1, nu)
+    alpha = 1 + rng.uniform(0.0, 2.0, size=(N, ncx))
+    J = rng.normal(size=(N, ncx, 12))
+    A, B = nat.jacobians(P.model, X, U)
+    args = (np.zeros((N - 1, 2 * nu)), np.zeros((N, ncx)), np.zeros(nx), 1.0, 1e-6)
+    r0 = nat.backward_pass(P.model, P.prob, X, U, alpha, J, A, B, *args)
+    r1 = nat.backward_pass(P.model, P.prob, X, U, alpha, np.ascontiguousarray(J.reshape(-1, 12).T), A, B, *args,
+                           soa=True)
+    for a, b in zip(r0, r1):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    with pytest.raises(ValueError):
+        nat.backward_pass(P.model, P.prob, X, U, alpha, J.reshape(-1, 12), A, B, *args, soa=True)
+
+
 @pytest.mark.parametrize("name", ["piano_mover", "quadrotor"])
 def test_pose_map_and_constraint_jacobian(name):
     from altro import _native, systems
