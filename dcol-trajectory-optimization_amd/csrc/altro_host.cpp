@@ -8,7 +8,8 @@
 //
 // Arithmetic follows the reference's expression order (numpy evaluates left to right,
 // no contraction: this file is compiled with -ffp-contract=off) so results agree with it
-// to rounding; 3-term dot products inside BLAS may differ in the last bit.
+// to rounding; the Riccati sweep's matrix products (mm / mtm) use explicit fused
+// multiply-adds, as the BLAS kernels behind numpy's matmul do.
 #include "../../include/dcol_altro.h"
 #include "altro_model.hpp"
 
@@ -61,7 +62,7 @@ __attribute__((always_inline)) inline void mm(int m, int p, int n, const double*
         for (int q = 0; q < p; ++q) {
             const double a = A[i * p + q];
             const double* b = B + q * n;
-            for (int j = 0; j < n; ++j) c[j] += a * b[j];
+            for (int j = 0; j < n; ++j) c[j] = std::fma(a, b[j], c[j]);
         }
     }
 }
@@ -74,7 +75,7 @@ __attribute__((always_inline)) inline void mtm(int p, int m, int n, const double
         for (int i = 0; i < m; ++i) {
             const double a = A[q * m + i];
             double* c = C + i * n;
-            for (int j = 0; j < n; ++j) c[j] += a * b[j];
+            for (int j = 0; j < n; ++j) c[j] = std::fma(a, b[j], c[j]);
         }
     }
 }
@@ -119,11 +120,28 @@ int backward_impl(int64_t T, int nx_, int nu_, const double* A, const double* B,
         }
         for (int i = 0; i < nu; ++i) kt[i] = Qu[i];
         chol_solve(L, nu, kt);
-        for (int j = 0; j < nx; ++j) {
-            double col[MU];
-            for (int i = 0; i < nu; ++i) col[i] = Qux[i * nx + j];
-            chol_solve(L, nu, col);
-            for (int i = 0; i < nu; ++i) Kt[i * nx + j] = col[i];
+        // K = Quu^-1 Qux: the nx right-hand sides side by side (row-major, the same
+        // per-column operation order as chol_solve, vectorised over the columns)
+        std::memcpy(Kt, Qux, sizeof(double) * nu * nx);
+        for (int i = 0; i < nu; ++i) {
+            double* ki = Kt + i * nx;
+            for (int q = 0; q < i; ++q) {
+                const double l = L[i * nu + q];
+                const double* kq = Kt + q * nx;
+                for (int j = 0; j < nx; ++j) ki[j] -= l * kq[j];
+            }
+            const double d = L[i * nu + i];
+            for (int j = 0; j < nx; ++j) ki[j] = ki[j] / d;
+        }
+        for (int i = nu - 1; i >= 0; --i) {
+            double* ki = Kt + i * nx;
+            for (int q = i + 1; q < nu; ++q) {
+                const double l = L[q * nu + i];
+                const double* kq = Kt + q * nx;
+                for (int j = 0; j < nx; ++j) ki[j] -= l * kq[j];
+            }
+            const double d = L[i * nu + i];
+            for (int j = 0; j < nx; ++j) ki[j] = ki[j] / d;
         }
         mm(nx, nu, nx, Bt, Kt, tmp);                       // B K
         for (int i = 0; i < nx * nx; ++i) Acl[i] = At[i] - tmp[i];
