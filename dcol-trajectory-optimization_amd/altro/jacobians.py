@@ -84,6 +84,8 @@ class DeviceJacobians:
         self.collect()
 
     def submit(self, X, U):
+        if self._pending:   # the kernel reads the pinned inputs this would overwrite
+            raise RuntimeError("submit() while the previous batch is in flight: collect() it first")
         self._x[:] = np.asarray(X, dtype=np.float64).reshape(-1, self.model.nx)[: self.T]
         self._u[:] = np.asarray(U, dtype=np.float64).reshape(self.T, self.model.nu)
         _native._check(self._fn(*self._args), "dcol_altro_jacobians_device")
