@@ -1031,14 +1031,15 @@ struct Solver {
             DCOL_ISTAMP(it, 0);
             // ---- mu = s'z / deg and the exit test first (pdip.py:410-422, quirk Q3): the
             // iteration that returns does not build the normal matrix
-            double il[OR > 0 ? OR : 1], isz[OR > 0 ? OR : 1];   // orthant rows: 1 / s, 1 / (s z)
+            double isz[OR > 0 ? OR : 1];   // orthant rows: 1 / (s z); 1 / s = z / (s z) is formed at
+                                           // each use (ilv): one multiply instead of a register
+                                           // array live across the whole iteration
             double sz = 0.0;
 #pragma unroll
             for (int k = 0; k < OR; ++k) {
                 // one reciprocal for both (one Newton step: the iterate sequence is unchanged on
                 // every golden vector, -12 VALU instructions per iteration)
                 const double rsz = frcp1(s[k] * z[k]);
-                il[k] = z[k] * rsz;
                 isz[k] = rsz;
                 sz = fma(live<FULL>(k) ? s[k] : 0.0, z[k], sz);
             }
@@ -1062,12 +1063,10 @@ struct Solver {
             for (int j = 0; j < N; ++j)
 #pragma unroll
                 for (int c = j; c < N; ++c) Hm[j][c] = 0.0;
-            double dd[OR > 0 ? OR : 1];
 #pragma unroll
             for (int k = 0; k < OR; ++k) {
                 const double zk = z[k];
-                const double d = zk * il[k];              // W^-2 = z / s on the orthant
-                dd[k] = d;
+                const double d = zk * ilv(k, isz);        // W^-2 = z / s on the orthant
                 double g[N];
 #pragma unroll
                 for (int j = 0; j < N; ++j) g[j] = G[k][j] * d;
@@ -1114,7 +1113,7 @@ struct Solver {
             double dsS[SSA * SD], dzS[SSA * SD];         // SOC rows of the affine step
             double dx[N];
             double cmax = 1.0, p1 = 0.0, p2 = 0.0;
-            predictor<FULL>(so, il, F, idg, dx, cp, dsS, dzS, cmax, p1, p2, dd);
+            predictor<FULL>(so, isz, F, idg, dx, cp, dsS, dzS, cmax, p1, p2);
             soc_bound(so, dsS, dzS, cmax);
             const double aa = frcp1(R::max(cmax));                   // quirk Q5 (no 0.99)
             DCOL_ISTAMP(it, 3);
@@ -1146,15 +1145,15 @@ struct Solver {
             const double smu = sigma * mu;
             double sbzt[SSA][SD], slds[SSA][SD];
             DCOL_ISTAMP(it, 4);
-            rhs_solve(so, il, F, idg, cp, smu, dx, sbzt, slds);
+            rhs_solve(so, isz, F, idg, cp, smu, dx, sbzt, slds);
             DCOL_ISTAMP(it, 5);
             cmax = 1.0;
             double cu[OR > 0 ? OR : 1], cdz[OR > 0 ? OR : 1];   // G dx and dz, kept for the update
 #pragma unroll
             for (int k = 0; k < OR; ++k) {
                 double dsk, num;
-                orth_step(k, il, cp, smu, dx, cu[k], cdz[k], dsk, num);
-                cmax = bound_inv(cmax, dsk, il[k]);
+                orth_step(k, isz, cp, smu, dx, cu[k], cdz[k], dsk, num);
+                cmax = bound_inv(cmax, dsk, ilv(k, isz));
                 cmax = bound_inv(cmax, num, isz[k]);       // -dz / z = -num / (s z)
             }
             double sdz[SSA][SD], sds[SSA][SD], su[SSA][SD];
@@ -1201,9 +1200,10 @@ struct Solver {
     // rx = G'z + c is folded into the same row sums: -rx + G'(W^-1 b~z) = G'(W^-1 b~z - z) - c,
     // and on an orthant row (W^-1 b~z)_k - z_k = -(z (s + r) + smu - cp) / s  (one G'v pass
     // per right-hand side, no separate G'z accumulation).
-    DCOL_HD void rhs_solve(const SocState* so, const double* il, const double (&F)[N][N], const double (&idg)[N],
-                           const double* cp, double smu, double* dx, double (*sbzt)[SD], double (*slds)[SD],
-                           const double* dd = nullptr) const {
+    // 1 / s of orthant row k from 1 / (s z) (the iteration's one reciprocal per row)
+    DCOL_HD double ilv(int k, const double* isz) const { return z[k] * isz[k]; }
+    DCOL_HD void rhs_solve(const SocState* so, const double* isz, const double (&F)[N][N], const double (&idg)[N],
+                           const double* cp, double smu, double* dx, double (*sbzt)[SD], double (*slds)[SD]) const {
         double rhs[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) rhs[j] = 0.0;
@@ -1211,7 +1211,7 @@ struct Solver {
         for (int k = 0; k < OR; ++k) {
             // (W^-1 b~z)_k - z_k; the predictor's -(z (s + r)) / s reuses W^-2 = z / s of the
             // normal matrix (dd)
-            const double t = (dd && !cp) ? -(dd[k] * (s[k] + r[k])) : -orth_num(k, cp, smu, s[k] + r[k]) * il[k];
+            const double t = !cp ? -((z[k] * ilv(k, isz)) * (s[k] + r[k])) : -orth_num(k, cp, smu, s[k] + r[k]) * ilv(k, isz);
 #pragma unroll
             for (int j = 0; j < N; ++j) rhs[j] += G[k][j] * t;
         }
@@ -1240,11 +1240,11 @@ struct Solver {
     // reference's dz = W^-1(W^-1 u - b~z), ds = W(lds - W dz) reduce exactly to
     //   dz = (z (u + r) + smu - cp) / s,   ds = -(s + r) - u   (u = G_k dx, r = G_k x - h_k),
     // i.e. the primal and complementarity rows of the same Newton system, in fewer operations.
-    DCOL_HD void orth_step(int k, const double* il, const double* cp, double smu, const double* dx, double& u,
+    DCOL_HD void orth_step(int k, const double* isz, const double* cp, double smu, const double* dx, double& u,
                            double& dz, double& ds, double& num) const {
         u = rowdot(k, dx);
         num = orth_num(k, cp, smu, u + r[k]);
-        dz = num * il[k];
+        dz = num * ilv(k, isz);
         ds = -(s[k] + r[k]) - u;
     }
     // one SOC block of the step: dz = W^-1(W^-1 u - b~z) = W^-2 u - W^-1 b~z (wbz), and
@@ -1267,18 +1267,18 @@ struct Solver {
     // ds/dz are not kept -- only cp = ds o dz (the corrector's cross term) and the sums
     // p1 = s'dz + z'ds, p2 = ds'dz that rho needs.  SOC rows keep ds/dz (dsS, dzS).
     template <bool FULL>
-    DCOL_HD void predictor(const SocState* so, const double* il, const double (&F)[N][N], const double (&idg)[N],
+    DCOL_HD void predictor(const SocState* so, const double* isz, const double (&F)[N][N], const double (&idg)[N],
                            double* dx, double* cp, double* dsS, double* dzS, double& cmax,
-                           double& p1, double& p2, const double* dd = nullptr) const {
+                           double& p1, double& p2) const {
         double sbzt[SSA][SD], slds[SSA][SD];
-        rhs_solve(so, il, F, idg, nullptr, 0.0, dx, sbzt, slds, dd);
+        rhs_solve(so, isz, F, idg, nullptr, 0.0, dx, sbzt, slds);
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
             const double u = rowdot(k, dx);
-            const double t = (u + r[k]) * il[k];
+            const double t = (u + r[k]) * ilv(k, isz);
             const double dz = z[k] * t;
             const double ds = -(s[k] + r[k]) - u;
-            cmax = bound_inv(cmax, ds, il[k]);
+            cmax = bound_inv(cmax, ds, ilv(k, isz));
             cmax = fmax(cmax, -t);
             const double c = ds * dz;
             cp[k] = c;
