@@ -359,7 +359,7 @@ static int pdip(const Prob* P, double tol, double* x, double* s, double* z, int*
         s[k] = t - P->h[k];
     }
     bring2cone(&W, s);
-    double yx[NMAX], xz[NMAX];
+    double yx[NMAX] = {0}, xz[NMAX];
     for (int j = 0; j < n; ++j) yx[j] = -P->c[j] / L[j][j];   /* quirk Q1 */
     bwd(n, L, yx, xz);
     for (int k = 0; k < m; ++k) {
