@@ -467,6 +467,29 @@ def run_mixed(args, world, rank, local, dev, coll_dev, dist):
         dist.destroy_process_group()
 
 
+def native_comm(NativeComm, dist, world, rank, local):
+    """(communicator, error) for the C-ABI RCCL path.  Rank 0 makes the unique id and ALWAYS
+    takes part in its broadcast (None when it could not make one), so a failure on rank 0
+    never leaves the other ranks in a collective rank 0 skipped; the ranks then all create
+    the communicator or all skip it.  (A failure inside ncclCommInitRank itself cannot be
+    signalled to the ranks already waiting in it; the usual failure -- librccl not
+    loadable -- surfaces in the id step.)"""
+    uid, err = [None], None
+    if rank == 0:
+        try:
+            uid = [NativeComm.unique_id()]
+        except Exception as e:
+            err = f"{type(e).__name__}: {e}"
+    if dist is not None:
+        dist.broadcast_object_list(uid, src=0)
+    if uid[0] is None:
+        return None, err or "rank 0 could not create a communicator id"
+    try:
+        return NativeComm(uid[0], world, rank, local), None
+    except Exception as e:   # recorded in the line; the step then uses torch.distributed
+        return None, f"{type(e).__name__}: {e}"
+
+
 def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
     """BASELINE configs[4]: 1M mixed-primitive pairs sharded over the ranks (class-balanced
     round-robin, dcol_amd.dist.shard_indices), each shard solved on its GPU from
@@ -499,13 +522,7 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
     comm, path = None, "torch.distributed all_gather_into_tensor" if dist is not None else "local copy (world 1)"
     native_error = None
     if args.backend == "nccl" and not args.torch_gather:
-        try:
-            uid = [NativeComm.unique_id() if rank == 0 else None]
-            if dist is not None:
-                dist.broadcast_object_list(uid, src=0)
-            comm = NativeComm(uid[0], world, rank, local)
-        except Exception as e:   # recorded in the line; the step then uses torch.distributed
-            comm, native_error = None, f"{type(e).__name__}: {e}"
+        comm, native_error = native_comm(NativeComm, dist, world, rank, local)
         if dist is not None:     # every rank takes the same path
             ok = torch.tensor([0.0 if comm is None else 1.0], device=coll_dev)
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
@@ -525,14 +542,17 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
         # state); the one-stream rate is reported beside it
         comms = [comm]
         for _ in range(max(1, args.streams) - 1):
-            try:
-                uid = [NativeComm.unique_id() if rank == 0 else None]
-                if dist is not None:
-                    dist.broadcast_object_list(uid, src=0)
-                comms.append(NativeComm(uid[0], world, rank, local))
-            except Exception as e:
-                native_error = f"extra stream communicator: {type(e).__name__}: {e}"
+            c, err = native_comm(NativeComm, dist, world, rank, local)
+            if dist is not None:     # decided together: no rank may go on to another id broadcast alone
+                ok = torch.tensor([0.0 if c is None else 1.0], device=coll_dev)
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+                if ok.item() < 1.0 and c is not None:
+                    c.close()
+                    c, err = None, err or "another rank could not create its communicator"
+            if c is None:
+                native_error = f"extra stream communicator: {err}"
                 break
+            comms.append(c)
         if dist is not None:     # every rank uses the same number of lanes
             t = torch.tensor([float(len(comms))], device=coll_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MIN)

@@ -122,3 +122,60 @@ def test_gloo_world2_hip_engine_gather_equals_single(balanced):
     np.testing.assert_array_equal(full["alpha"], ref.alpha)
     np.testing.assert_array_equal(full["grad"], ref.grad)
     np.testing.assert_array_equal(full["status"], d["status"][:120])
+
+
+class _FakeComm:
+    """Stand-in for dcol_amd.dist.NativeComm (no RCCL on the CPU): ``fail`` names the step
+    that raises -- "id" (rank 0's unique id) or "create" (the constructor on rank 1)."""
+    fail = None
+
+    def __init__(self, uid, world, rank, device):
+        if _FakeComm.fail == "create" and rank == 1:
+            raise RuntimeError("ncclCommInitRank: stand-in failure")
+        self.uid, self.rank = uid, rank
+
+    @staticmethod
+    def unique_id():
+        if _FakeComm.fail == "id":
+            raise RuntimeError("librccl not loadable (stand-in)")
+        return b"\x07" * 128
+
+
+def _comm_worker(rank, world, port, fail, q):
+    import sys
+    import torch.distributed as dist
+    from conftest import REPO
+    if REPO not in sys.path:
+        sys.path.insert(0, REPO)
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _FakeComm.fail = fail
+    c, err = bench.native_comm(_FakeComm, dist, world, rank, 0)
+    dist.barrier()                 # reached by both ranks: no collective was left unmatched
+    q.put((rank, c is not None, c.uid if c is not None else None, err))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail", [None, "id", "create"])
+def test_native_comm_setup_never_splits_collectives(fail):
+    """bench.native_comm: rank 0 takes part in the id broadcast even when it cannot make an
+    id, so a failure there ends with every rank skipping the C-ABI path instead of one rank
+    waiting in a broadcast the other skipped (world 2, gloo)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, 2, port, fail, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    if fail is None:
+        assert all(ok for _, ok, _, _ in res) and res[0][2] == res[1][2] == b"\x07" * 128
+    elif fail == "id":
+        assert not any(ok for _, ok, _, _ in res)
+        assert "librccl" in res[0][3] and "rank 0" in res[1][3]
+    else:   # the caller's all-reduce of the outcome then makes rank 0 drop its communicator
+        assert res[0][1] and not res[1][1] and "stand-in" in res[1][3]
