@@ -159,7 +159,9 @@ def main():
                     help="timed steps (0.05-2 ms each; enough for the GPU clocks to settle)")
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--pairs", type=int, default=100_000, help="pairs per GPU")
-    ap.add_argument("--grad", choices=["fd", "envelope"], default="fd")
+    ap.add_argument("--grad", choices=["fd", "envelope", "implicit"], default="fd",
+                    help="fd: the reference's formulation (the headline); envelope / implicit: the closed-form "
+                         "and implicit-function modes (DESIGN.md section 3 \"Gradient modes\")")
     ap.add_argument("--cpu-sample", type=int, default=16000)
     ap.add_argument("--cpu-workers", type=int, default=0,
                     help="host processes / threads for the CPU baselines (0 = every core this process may run on)")
@@ -337,6 +339,10 @@ def main():
         sel = np.unique(np.concatenate([np.arange(n // 2), np.arange(B - (n - n // 2), B)]))
         ref = O.run_batch(tab, s1[sel], s2[sel], p1[sel], p2[sel], 1e-6, True)
         ok = ref["status"] == 0
+        if args.grad == "implicit":
+            # checked against the oracle's restatement of the implicit mode (the reference
+            # has none), on a sub-sample (its dG / dh are central differences)
+            sel, ref, ok = implicit_reference(O, tab, s1, s2, p1, p2, sel[:: max(1, sel.size // 64)])
         a_ok = np.all(np.abs(alpha[sel][ok] - ref["alpha"][ok]) <= 1e-6 * np.abs(ref["alpha"][ok]) + 1e-12)
         g_ok = np.all(np.abs(grad[:, sel].T[ok] - ref["grad"][ok]).max(1)
                       <= 1e-5 * np.maximum(np.abs(ref["grad"][ok]).max(1), 1))
@@ -664,7 +670,8 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
             "pairs": int(k), "status_equal": bool(np.array_equal(status[:k], ref["status"])),
             "alpha_ok": bool(np.all(np.abs(full[:k, 0][ok] - ref["alpha"][ok]) <= 1e-6 * np.abs(ref["alpha"][ok]) + 1e-12)),
             "grad_ok": bool(np.all(np.abs(full[:k, 1:13][ok] - ref["grad"][ok]).max(1)
-                                   <= 1e-5 * np.maximum(np.abs(ref["grad"][ok]).max(1), 1)))}
+                                   <= 1e-5 * np.maximum(np.abs(ref["grad"][ok]).max(1), 1)))
+            if args.grad == "fd" else None}   # the C oracle restates the reference's FD gradient only
     return line
 
 
@@ -684,7 +691,7 @@ def mixed_flops(tab, s1, s2, iters, status, grad="fd"):
             if not m.any():
                 continue
             c = classes[f"{names[a]}-{names[b]}"]
-            g = c["grad_fd"] if grad == "fd" else 760
+            g = GRAD_OPS.get(grad, c["grad_fd"])   # closed-form modes: the poly x poly hand counts
             total += m.sum() * (c["assembly"] + c["pdip_fixed"] + g) + c["pdip_per_iter"] * iters[m].sum()
     return total
 
@@ -751,6 +758,17 @@ def altro_section():
     return out
 
 
+def implicit_reference(O, tab, s1, s2, p1, p2, sel):
+    """(sel, ref, ok) for the parity check of --grad implicit: alpha / status from the oracle's
+    proximity, the gradient from its implicit_gradient restatement at the returned iterate."""
+    alpha, grad, status = np.zeros(sel.size), np.zeros((sel.size, 12)), np.zeros(sel.size, np.int32)
+    for j, i in enumerate(sel):
+        a, b = O.shape_from_table(tab, s1[i]), O.shape_from_table(tab, s2[i])
+        alpha[j], _, x, s_, z, _, dims = O.proximity(a, p1[i][:3], p1[i][3:], b, p2[i][:3], p2[i][3:], 1e-6)
+        grad[j] = O.implicit_gradient(a, b, x, s_, z, np.concatenate([p1[i], p2[i]]), dims)
+    return sel, {"alpha": alpha, "grad": grad, "status": status}, status == 0
+
+
 def flops_per_pair(iters, grad="fd", cls="polytope-polytope (bench configs[3])"):
     """Algorithmic FP64 operation count per pair (each +, -, *, /, sqrt = 1) at the run's
     mean Newton iteration count.  Official counts: the op-counting build of
@@ -763,8 +781,17 @@ def flops_per_pair(iters, grad="fd", cls="polytope-polytope (bench configs[3])")
     path = os.path.join(REPO, "profiles", "flop_model.json")
     if os.path.exists(path):
         c = json.load(open(path))["classes"][cls]
-        return c["assembly"] + c["pdip_fixed"] + it * c["pdip_per_iter"] + (c["grad_fd"] if grad == "fd" else 760)
-    return 530 + 777 + it * 1682 + 276 + (8485 if grad == "fd" else 760)
+        return c["assembly"] + c["pdip_fixed"] + it * c["pdip_per_iter"] + GRAD_OPS.get(grad, c["grad_fd"])
+    return 530 + 777 + it * 1682 + 276 + GRAD_OPS.get(grad, 8485)
+
+
+# hand counts of the closed-form gradient modes for poly6 x poly6 (no reference counterpart,
+# so no counted restatement): envelope = env_grad_prim x 2 = 760; implicit (dcol_device.hpp
+# Solver::implicit_weights, imp_grad_prim) = normal matrix at the returned iterate 12 rows x
+# 28 (336) + 4 x 4 Cholesky (40) + solve v = H^-1 e3 (32) + weights a = -W^-2 G v 12 x 8 (96)
+# + two row aggregates per primitive 12 x 2 x 6 (144) + the envelope pass (760) + the dG-only
+# pass at v, 2 x 170 (340) = 1,748
+GRAD_OPS = {"envelope": 760, "implicit": 1748}
 
 
 if __name__ == "__main__":
