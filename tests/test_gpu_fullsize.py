@@ -227,3 +227,36 @@ def test_codegen_invariance_mixed(tmp_path):
     difference is a machine-code defect -- the class of fault that made the 326f844 build
     of the (6, 1, 12) LPP-2 ball kernel drift."""
     _assert_bitwise(_mixed_outputs(tmp_path, "product"), _mixed_outputs(tmp_path, "xcheck", lib=XCHECK_LIB))
+
+
+def test_max_size_192m_pairs_position_independent():
+    """Maximum-size launch: 192M pairs in ONE plan (192 copies of a 1M batch of the benchmark
+    distribution; 18 GB of poses and 18 GB of gradients in HBM, so pose / gradient offsets
+    run past 2^31 elements -- int64 indexing end to end).  There is no cross-pair arithmetic, so every copy must equal the
+    1M solve bitwise -- status, iteration counts, alpha and gradient -- wherever it sits in
+    the batch (compared on the device)."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import torch
+
+    import bench
+    from dcol_amd import Engine, spec_from_arrays
+    tab = bench.shape_table()
+    n, K = 1_000_000, 192
+    s1, s2, p1, p2 = bench.pairs(n, len(tab["type"]), seed=11)
+    eng = Engine(device=0)
+    ids = np.array([eng.register(spec_from_arrays(tab, k)) for k in range(len(tab["type"]))], np.int32)
+    dev = torch.device("cuda", 0)
+    d1 = torch.from_numpy(np.ascontiguousarray(p1.T)).to(dev)
+    d2 = torch.from_numpy(np.ascontiguousarray(p2.T)).to(dev)
+    base = eng.plan(ids[s1], ids[s2], cache=False).run(d1, d2, grad="fd", contact=False)
+    assert bool((base["status"] == 0).all())
+    big = eng.plan(np.tile(ids[s1], K), np.tile(ids[s2], K), cache=False).run(
+        d1.repeat(1, K).contiguous(), d2.repeat(1, K).contiguous(), grad="fd", contact=False)
+    assert big["grad"].shape == (12, n * K) and n * K * 12 > 2 ** 31
+    for k in range(K):
+        sl = slice(k * n, (k + 1) * n)
+        assert torch.equal(big["status"][sl], base["status"]), k
+        assert torch.equal(big["iters"][sl], base["iters"]), k
+        assert torch.equal(big["alpha"][sl], base["alpha"]), k
+        assert torch.equal(big["grad"][:, sl], base["grad"]), k
