@@ -144,6 +144,9 @@ class ObstacleField:
         the pinned buffer and the phase (H2D -> solve -> D2H) is queued on self.stream; the
         host is free until collect().  One phase in flight at a time."""
         import torch
+        if self._pending is not None:
+            # the running phase may still read h_pose1 (zero_copy) or write h_out
+            raise RuntimeError("submit() while a phase is in flight: collect() it first")
         P = np.asarray(victim_poses, dtype=np.float64).reshape(self.N, 6)
         self._hp3[:] = P.T[:, :, None]          # pose of knot t for each of its n_obs pairs
         direct = self._direct.get(bool(grad))
@@ -156,6 +159,8 @@ class ObstacleField:
         # stream synchronised in collect) whatever stream context the caller is in
         with torch.cuda.stream(self.stream):
             if graph is not None:
+                graph.replay()
+            else:
                 self.pose1.copy_(self.h_pose1, non_blocking=True)
                 self._launch[bool(grad)]()
                 n = 14 * self.B if grad else 2 * self.B  # alpha-only phases skip the gradient block
@@ -164,10 +169,12 @@ class ObstacleField:
 
     soa_grad = True   # collect(soa=True): gradients in the engine's [12, N n_obs] layout
 
-    def collect(self, soa=False):
+    def collect(self, soa=False, raise_=True):
         """Wait for the phase started by submit() -> (alpha [N, n_obs], J [N, n_obs, 12] |
         None), or J [12, N n_obs] with soa=True (no transpose).  Raises like the reference on
-        the first failed pair (knot-major order)."""
+        the first failed pair (knot-major order); with raise_=False returns (alpha, J,
+        status [N, n_obs]) instead and leaves the decision to the caller (a batch of several
+        line-search trials, where only the trials the reference would evaluate count)."""
         grad = self._pending
         self._pending = None
         if grad is None:
@@ -176,19 +183,21 @@ class ObstacleField:
         self.batches += 1
         self.pairs += self.B
         st = self._np_status
-        if st.any():
+        if raise_ and st.any():
             raise_for_status(int(st[np.flatnonzero(st)[0]]))
         alpha = self._np_alpha.reshape(self.N, self.n_obs).copy()
         if not grad:
             J = None
         else:
             J = self._np_grad.copy() if soa else self._np_grad.T.reshape(self.N, self.n_obs, 12).copy()
+        if not raise_:
+            return alpha, J, st.reshape(self.N, self.n_obs).copy()
         return alpha, J
 
-    def evaluate(self, victim_poses, grad: bool):
+    def evaluate(self, victim_poses, grad: bool, raise_=True):
         """submit() + collect()."""
         self.submit(victim_poses, grad)
-        return self.collect()
+        return self.collect(raise_=raise_)
 
 
 __all__ = ["ObstacleField", "PDIPFailure"]

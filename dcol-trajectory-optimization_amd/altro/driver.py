@@ -36,6 +36,8 @@ import time
 
 import numpy as np
 
+from dcol_amd.engine import raise_for_status
+
 from . import _native
 from . import jacobians as _jacobians
 from . import systems as _systems
@@ -95,14 +97,16 @@ class _Timed:
         """the evaluator returns gradients in the engine's component-major layout on request"""
         return self.async_ and getattr(self.field, "soa_grad", False)
 
-    def collect(self):
+    def collect(self, raise_=True):
+        """-> (alpha, J), or (alpha, J, status) with raise_=False (see ObstacleField.collect)."""
         t0 = time.perf_counter()
         poses, grad = self._job
         self._job = None
+        kw = {} if raise_ else {"raise_": False}
         if self.soa:
-            out = self.field.collect(soa=True)
+            out = self.field.collect(soa=True, **kw)
         else:
-            out = self.field.collect() if self.async_ else self.field.evaluate(poses, grad)
+            out = self.field.collect(**kw) if self.async_ else self.field.evaluate(poses, grad, **kw)
         self.seconds += time.perf_counter() - t0
         self.batches += 1
         self.pairs += poses.shape[0] * out[0].shape[1]
@@ -234,16 +238,21 @@ def solve(params, X, U, prox=None, engine=None, verbose=True, prox_wide=None) ->
                 continue
             # retries: the next TRIALS step lengths of the reference's halving sequence in
             # one batch; the first one that lowers the cost is taken, exactly as trying them
-            # one at a time would (later ones are discarded)
+            # one at a time would (later ones are discarded).  A failed pair raises only when
+            # its trial is the one being evaluated: trials after the accepted one, or past
+            # max_linesearch_iters, are never looked at by the reference.
             w = min(TRIALS, n_ls - tried)
             steps = [a * 0.5 ** j for j in range(TRIALS)]
             Xs, Us = _native.rollouts(P.model, X, U, K, k, steps)
             wide.submit(_native.victim_poses(P.model, Xs.reshape(-1, nx)), True)
-            ans, Jns = wide.collect()
+            ans, Jns, sts = wide.collect(raise_=False)
             ans = ans.reshape(TRIALS, N, ncx)
+            sts = sts.reshape(TRIALS, N * ncx)
             if not wide.soa:
                 Jns = Jns.reshape(TRIALS, N, ncx, 12)
             for j in range(w):
+                if sts[j].any():            # knot-major first failure of this trial
+                    raise_for_status(int(sts[j][np.flatnonzero(sts[j])[0]]))
                 hxn = 1 - ans[j]
                 new = P.cost(Xs[j], Us[j], hxn, mu, mux, lam, rho)
                 tried += 1

@@ -46,28 +46,27 @@ class OracleField:
         self.tol = tol
         self.threads = threads or min(8, os.cpu_count() or 1)
 
-    def evaluate(self, victim_poses, grad):
+    def _solve(self, p1, grad):
+        return c_oracle.run_batch(self.tab, self.s1, self.s2, p1, self.pose2, tol=self.tol, want_grad=grad,
+                                  threads=self.threads)
+
+    def evaluate(self, victim_poses, grad, raise_=True):
+        """-> (alpha, J), or (alpha, J, status) with raise_=False (ObstacleField.collect)."""
         p1 = np.repeat(np.asarray(victim_poses, dtype=np.float64).reshape(self.N, 6), self.n_obs, axis=0)
-        out = c_oracle.run_batch(self.tab, self.s1, self.s2, p1, self.pose2, tol=self.tol, want_grad=grad,
-                                 threads=self.threads)
+        out = self._solve(p1, grad)
         st = out["status"]
-        if st.any():
+        if raise_ and st.any():
             raise_for_status(int(st[np.flatnonzero(st)[0]]))
         alpha = out["alpha"].reshape(self.N, self.n_obs)
         J = out["grad"].reshape(self.N, self.n_obs, 12) if grad else None
+        if not raise_:
+            return alpha, J, np.asarray(st).reshape(self.N, self.n_obs)
         return alpha, J
 
 
 class NumpyOracleField(OracleField):
     """Same, solved by the NumPy restatement (bit-exact with the reference; slow)."""
 
-    def evaluate(self, victim_poses, grad):
+    def _solve(self, p1, grad):
         from oracle import dcol_oracle
-        p1 = np.repeat(np.asarray(victim_poses, dtype=np.float64).reshape(self.N, 6), self.n_obs, axis=0)
-        out = dcol_oracle.run_batch(self.tab, self.s1, self.s2, p1, self.pose2, tol=self.tol, want_grad=grad)
-        st = out["status"]
-        if st.any():
-            raise_for_status(int(st[np.flatnonzero(st)[0]]))
-        alpha = out["alpha"].reshape(self.N, self.n_obs)
-        J = out["grad"].reshape(self.N, self.n_obs, 12) if grad else None
-        return alpha, J
+        return dcol_oracle.run_batch(self.tab, self.s1, self.s2, p1, self.pose2, tol=self.tol, want_grad=grad)

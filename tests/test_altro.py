@@ -203,6 +203,66 @@ def test_altro_wide_line_search_matches_reference_cpu_evaluator():
     assert r.prox_batches == 1 + int(np.sum(1 + np.ceil((trials - 1) / TRIALS)))
 
 
+def _poisoned_wide(params, N, golden_alpha, poison_accepted):
+    """A wide (TRIALS-trajectory) oracle evaluator that marks every pair of the trials the
+    reference never evaluates (after the accepted one) as failed (MAXITER); with
+    poison_accepted the accepted trial itself fails instead."""
+    from altro.driver import TRIALS
+    from altro_cpu import OracleField
+    from dcol_amd import _lib
+    # per retry batch: index of the accepted trial in it (None: all TRIALS tried, none accepted)
+    plan = []
+    n_ls = int(params["max_linesearch_iters"])
+    for a in golden_alpha:
+        if a == 0:                          # failed line search: every batch tried, none accepted
+            plan += [None] * (-(-(n_ls - 1) // TRIALS))
+            continue
+        t = int(round(np.log2(1 / a))) + 1
+        if t == 1:
+            continue
+        nb = -(-(t - 1) // TRIALS)
+        plan += [None] * (nb - 1) + [(t - 2) % TRIALS]
+
+    class Poisoned(OracleField):
+        batch = 0
+
+        def evaluate(self, poses, grad, raise_=True):
+            a, J, st = super().evaluate(poses, grad, raise_=False)
+            j_acc = plan[Poisoned.batch]
+            Poisoned.batch += 1
+            st = st.reshape(TRIALS, -1).copy()
+            if j_acc is not None:
+                if poison_accepted:
+                    st[j_acc, 7] = _lib.MAXITER
+                else:
+                    st[j_acc + 1:] = _lib.MAXITER
+            st = st.reshape(a.shape)
+            if raise_ and st.any():
+                from dcol_amd.engine import raise_for_status
+                raise_for_status(int(st.ravel()[np.flatnonzero(st)[0]]))
+            return (a, J) if raise_ else (a, J, st)
+    return Poisoned(params["P_vic"], params["P_obs"], TRIALS * N)
+
+
+def test_wide_line_search_ignores_failures_of_unevaluated_trials():
+    """a retry batch solves TRIALS step lengths at once; a failure in a trial the
+    reference would never evaluate (after the accepted one) must not abort the run, while a
+    failure in the accepted trial raises like the reference (PDIPFailure, pdip.py:470)."""
+    from altro import solve, systems
+    from altro_cpu import OracleField
+    from dcol_amd.engine import PDIPFailure
+    g = np.load(os.path.join(GOLDEN, "altro", "altro_quadrotor.npz"))
+    params, X, U = systems.initialize("quadrotor")
+    N = params["N"]
+    r = solve(params, X, U, prox=OracleField(params["P_vic"], params["P_obs"], N),
+              prox_wide=_poisoned_wide(params, N, g["alpha"], False), verbose=False)
+    check_run(r, g)
+    params, X, U = systems.initialize("quadrotor")
+    with pytest.raises(PDIPFailure):
+        solve(params, X, U, prox=OracleField(params["P_vic"], params["P_obs"], N),
+              prox_wide=_poisoned_wide(params, N, g["alpha"], True), verbose=False)
+
+
 def test_reg_max_raises_like_reference():
     """update_reg (ALTRO.py:51-74): a failed line search at reg == reg_max is a ValueError."""
     from altro import solve, systems
@@ -276,20 +336,44 @@ def test_obstacle_field_phase_modes_bitwise_equal(name, monkeypatch):
         pytest.skip("no GPU")
     from altro import systems
     from altro.constraints import ObstacleField
+    from altro_cpu import OracleField
+    from conftest import alpha_close, grad_close
     params, X, U = systems.initialize(name)
     mod = systems.get(name)
     rng = np.random.default_rng(4)
-    Xs = np.array(params["Xref"], dtype=np.float64) + 0.05 * rng.normal(size=(params["N"], params["nx"]))
-    poses = mod.victim_poses(params, Xs)
+    poses = [mod.victim_poses(params, np.array(params["Xref"], dtype=np.float64)
+                              + 0.05 * rng.normal(size=(params["N"], params["nx"]))) for _ in range(3)]
+    cpu = OracleField(params["P_vic"], params["P_obs"], params["N"])
+    want = [cpu.evaluate(p, True) for p in poses]
+
+    class Counting:
+        """graph proxy counting replays (graph mode must replay its captured graph)"""
+        def __init__(self, g):
+            self.g, self.n = g, 0
+
+        def replay(self):
+            self.n += 1
+            self.g.replay()
+
     outs = {}
     for mode in ("zero_copy", "graph", "eager"):
         monkeypatch.setenv("DCOL_ALTRO_PHASE", mode)
         f = ObstacleField(params["P_vic"], params["P_obs"], params["N"])
+        f._graphs = {k: Counting(g) for k, g in f._graphs.items()}
         outs[mode] = []
-        for g in (True, False, True):
-            f.submit(poses, g)
+        for i, g in enumerate((True, False, True)):
+            f.h_out.fill_(float("nan"))              # stale outputs must never come back
+            f.submit(poses[i], g)
+            with pytest.raises(RuntimeError, match="in flight"):
+                f.submit(poses[i], g)
             outs[mode].append(f.collect())
         assert f.mode == mode or (mode == "zero_copy" and f.mode == "graph")
+        if f.mode == "graph":
+            assert f._graphs[True].n == 2 and f._graphs[False].n == 1
+        for i, (a, J) in enumerate(outs[mode]):      # every mode against the oracle
+            assert alpha_close(a, want[i][0]).all(), mode
+            if J is not None:
+                assert grad_close(J.reshape(-1, 12), want[i][1].reshape(-1, 12)).all(), mode
     for mode in ("graph", "eager"):
         for (a, J), (b, K) in zip(outs["zero_copy"], outs[mode]):
             assert np.array_equal(a, b)
