@@ -122,6 +122,7 @@ struct dcol_table {
 struct Launch {
     int kind;       // 0 = solve, 1 = reject
     int N, nsoc, omax, lpp;
+    int oe = 0;          // row-partitioned bucket (extra-row slots; 0: dense-row kernels)
     bool full = false;   // every pair has o == omax: the padding-free kernel (DCOL_FULL_VARIANTS) if built
     bool ball = false;   // every SOC block is a ball block: the structured kernel (DCOL_BALL_VARIANTS) if built
     bool cone = false;   // every SOC block is a cone block (N = 4): DCOL_CONE_VARIANTS if built
@@ -156,7 +157,14 @@ struct dcol_plan {
 
 namespace {
 
-hipError_t launch_variant(int N, int nsoc, int omax, int lpp, int flags, const KArgs& a, hipStream_t st) {
+hipError_t launch_variant(int N, int nsoc, int omax, int lpp, int flags, const KArgs& a, hipStream_t st, int oe = 0) {
+    if (oe > 0) {
+        if (N == 5 && nsoc == 1) return launch_part_n5s1(omax, oe, lpp, flags, a, st);
+        if (N == 5 && nsoc == 2) return launch_part_n5s2(omax, oe, lpp, flags, a, st);
+        if (N == 6 && nsoc == 1) return launch_part_n6s1(omax, oe, lpp, flags, a, st);
+        if (N == 6 && nsoc == 2) return launch_part_n6s2(omax, oe, lpp, flags, a, st);
+        return hipErrorInvalidValue;
+    }
     if (N == 4) return launch_n4(nsoc, omax, lpp, flags, a, st);
     if (N == 5) return launch_n5(nsoc, omax, lpp, flags, a, st);
     if (N == 6) return launch_n6(nsoc, omax, lpp, flags, a, st);
@@ -287,6 +295,10 @@ bool cone_disabled() {
 // buckets up to twice its rows (a tight bucket compiled only with LPP 2 -- 6 or 10 rows --
 // loses to the next bucket's 8-lane groups), fewer rows on ties.
 void latency_config(Launch& L) {
+    if (L.oe > 0) {   // row-partitioned bucket: its largest compiled LPP
+        L.lpp = part_lpp(L.N, L.nsoc, L.omax, L.oe, true);
+        return;
+    }
     const int fl = L.ball ? 2 : (L.cone ? 4 : 0);
     int best_o = L.omax, best_l = max_lpp(L.N, L.nsoc, L.omax, fl);
     for (const int om : buckets().at({L.N, L.nsoc})) {
@@ -307,11 +319,14 @@ void latency_config(Launch& L) {
 // O(B): each distinct (shape1, shape2) is classified once (a dense S x S cache when S^2 is
 // at most 4M cells and small against B, else a hash map), then a stable counting sort by
 // group, groups in key order.
+// fused_part: a row-partitioned bucket is used only where the fused small-plan kernel has
+// its case (the retry of a small plan that would otherwise lose its single fused launch;
+// the other pairs take the dense-row kernels, which the fused kernel covers)
 int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, dcol_plan* p,
-                 std::vector<int32_t>& perm, bool case4) {
+                 std::vector<int32_t>& perm, bool case4, bool fused_part = false) {
     const int32_t ns = (int32_t)t->shapes.size();
-    // kind, N, nsoc, omax, lpp, ball (SOC blocks all balls: no cone), code
-    using Key = std::tuple<int, int, int, int, int, int, int>;
+    // kind, N, nsoc, omax, lpp, ball (SOC blocks all balls: no cone), code, oe (row partition)
+    using Key = std::tuple<int, int, int, int, int, int, int, int>;
     struct Group {
         Key key;
         bool full = true;   // every pair class of the group has o == omax
@@ -327,11 +342,16 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
         // (CONE kernels), 0 dense
         const bool none_cone = a.soc_kind != SOC_CONE && b.soc_kind != SOC_CONE;
         const bool all_cone = a.soc_kind != SOC_BALL && b.soc_kind != SOC_BALL;
+        if (fused_part && c.status == DCOL_OK && c.oe > 0 &&
+            fused_vid(c.N, c.nsoc, c.omax, part_lpp(c.N, c.nsoc, c.omax, c.oe, true),
+                      (none_cone && !ball_disabled()) ? LF_BALL : 0, c.oe) < 0)
+            c = classify(a, b, case4, false);
         const int ball = c.nsoc == 0 ? 0
                          : (none_cone && !ball_disabled()) ? 1
                          : (all_cone && c.N == 4 && !cone_disabled()) ? 2 : 0;
-        if (c.status == DCOL_OK && ball) c.lpp = choose_lpp(c.N, c.nsoc, c.omax, 2 * ball);   // flavour's own list
-        Key k = c.status == DCOL_OK ? Key{0, c.N, c.nsoc, c.omax, c.lpp, ball, 0} : Key{1, 0, 0, 0, 0, 0, c.status};
+        // flavour's own list (row-partitioned buckets have theirs: PairClass::lpp)
+        if (c.status == DCOL_OK && ball && c.oe == 0) c.lpp = choose_lpp(c.N, c.nsoc, c.omax, 2 * ball);
+        Key k = c.status == DCOL_OK ? Key{0, c.N, c.nsoc, c.omax, c.lpp, ball, 0, c.oe} : Key{1, 0, 0, 0, 0, 0, c.status, 0};
         auto it = gid_of_key.emplace(k, (int32_t)groups.size()).first;
         if (it->second == (int32_t)groups.size()) groups.push_back(Group{k});
         Group& g = groups[it->second];
@@ -366,6 +386,15 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
     p->B = B;
     p->launches.clear();
     perm.assign((size_t)B, 0);
+    // Latency configurations only when the whole plan cannot fill the GPU: the buckets of a
+    // large mixed plan run side by side on the fan-out streams, so each keeps its throughput
+    // configuration even when it alone would leave SIMDs idle (DCOL_LATENCY_PER_LAUNCH=1:
+    // the per-launch rule, for A/B runs).
+    static const bool per_launch = std::getenv("DCOL_LATENCY_PER_LAUNCH") != nullptr;
+    int64_t plan_lanes = 0;
+    for (const Group& G : groups)
+        if (std::get<0>(G.key) == 0) plan_lanes += G.n * std::get<4>(G.key);
+    const bool small_plan = plan_lanes < 64LL * t->simds;
     int64_t at = 0;
     for (auto& kv : gid_of_key) {   // key order
         Group& G = groups[kv.second];
@@ -377,13 +406,14 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
         L.omax = std::get<3>(G.key);
         L.lpp = std::get<4>(G.key);
         L.code = std::get<6>(G.key);
+        L.oe = std::get<7>(G.key);
         L.full = L.kind == 0 && G.full;
         L.ball = L.kind == 0 && std::get<5>(G.key) == 1;
         L.cone = L.kind == 0 && std::get<5>(G.key) == 2;
         L.slot0 = at;
         L.n = G.n;
-        if (L.kind == 0 && !lpp_forced() && L.n * L.lpp < 64LL * t->simds)   // cannot fill the GPU
-            latency_config(L);
+        if (L.kind == 0 && !lpp_forced() && L.n * L.lpp < 64LL * t->simds && (small_plan || per_launch))
+            latency_config(L);   // cannot fill the GPU
         at += G.n;
         p->launches.push_back(L);
     }
@@ -426,10 +456,12 @@ void assign_lanes(dcol_plan* p) {
 // than one wave per SIMD: every bucket already took its latency configuration) runs as ONE
 // fused launch; p->segs is left empty when it does not qualify (large or single-variant
 // plans, variants outside the fused kernel, DCOL_PLAN_NO_FUSE).
-void plan_fuse(const dcol_table* t, dcol_plan* p, bool allow) {
+// Returns 0 when fused (or not allowed), 1 when the plan does not qualify (large or
+// single-variant), 2 when it qualifies but a bucket has no case in the fused kernel.
+int plan_fuse(const dcol_table* t, dcol_plan* p, bool allow) {
     p->segs.clear();
     p->fused_blocks = 0;
-    if (!allow) return;
+    if (!allow) return 0;
     int solves = 0;
     int64_t lanes = 0;
     for (const Launch& L : p->launches)
@@ -437,19 +469,42 @@ void plan_fuse(const dcol_table* t, dcol_plan* p, bool allow) {
             ++solves;
             lanes += L.n * L.lpp;
         }
-    if (solves < 2 || solves > kMaxFusedSegs || lanes >= 64LL * t->simds) return;
+    if (solves < 2 || solves > kMaxFusedSegs || lanes >= 64LL * t->simds) return 1;
     std::vector<FusedSeg> segs;
     int64_t block = 0;
     for (const Launch& L : p->launches) {
         if (L.kind != 0) continue;
-        const int vid = fused_vid(L.N, L.nsoc, L.omax, L.lpp, L.flags());
-        if (vid < 0) return;
+        const int vid = fused_vid(L.N, L.nsoc, L.omax, L.lpp, L.flags(), L.oe);
+        if (vid < 0) return 2;
         segs.push_back(FusedSeg{vid, L.lpp, block, L.slot0, L.n});
         block += (L.n * L.lpp + kBlock - 1) / kBlock;
     }
     p->segs = std::move(segs);
     p->fused_blocks = block;
     p->lanes = 1;   // no fan-out
+    return 0;
+}
+
+// bucket + fuse; a small plan whose row-partitioned buckets lack fused cases is re-bucketed
+// with those pairs on the dense-row kernels, so it keeps its single launch (latency-bound
+// plans lose far more to a fan-out than the partition saves)
+// (the buckets do not depend on allow_fuse: a DCOL_PLAN_NO_FUSE plan launches the same
+// buckets one by one)
+int bucket_and_fuse(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, dcol_plan* p,
+                    std::vector<int32_t>& perm, bool case4, bool allow_fuse) {
+    int rc = bucket_pairs(t, B, s1, s2, p, perm, case4);
+    if (rc != DCOL_SUCCESS) return rc;
+    if (plan_fuse(t, p, true) == 2) {
+        rc = bucket_pairs(t, B, s1, s2, p, perm, case4, true);
+        if (rc != DCOL_SUCCESS) return rc;
+        plan_fuse(t, p, true);
+    }
+    if (!allow_fuse && p->fused()) {   // same buckets, launched one by one (fan-out)
+        p->segs.clear();
+        p->fused_blocks = 0;
+        assign_lanes(p);
+    }
+    return DCOL_SUCCESS;
 }
 
 int ensure_fanout(const dcol_table* tc, dcol_plan* p) {
@@ -480,12 +535,11 @@ int dcol_plan_create_ex(const dcol_table* t, int64_t B, const int32_t* s1, const
     auto* p = new (std::nothrow) dcol_plan();
     if (!p) return fail(DCOL_ERR_NOMEM, "host allocation failed");
     std::vector<int32_t> perm;
-    int rc = bucket_pairs(t, B, s1, s2, p, perm, (options & DCOL_PLAN_CASE4) != 0);
+    int rc = bucket_and_fuse(t, B, s1, s2, p, perm, (options & DCOL_PLAN_CASE4) != 0, (options & DCOL_PLAN_NO_FUSE) == 0);
     if (rc != DCOL_SUCCESS) {
         delete p;
         return rc;
     }
-    plan_fuse(t, p, (options & DCOL_PLAN_NO_FUSE) == 0);
     p->owns = true;
     if (B == 0) {
         *out = p;
@@ -591,7 +645,7 @@ int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, 
             hipLaunchKernelGGL(reject_kernel, dim3(grid), dim3(kBlock), 0, ls, a, L.code);
             e = hipGetLastError();
         } else {
-            e = launch_variant(L.N, L.nsoc, L.omax, L.lpp, L.flags(), a, ls);
+            e = launch_variant(L.N, L.nsoc, L.omax, L.lpp, L.flags(), a, ls, L.oe);
         }
         if (e != hipSuccess) break;
     }
@@ -611,6 +665,21 @@ int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, 
     return DCOL_SUCCESS;
 }
 
+#ifdef DCOL_CHECK_EXEC
+// diagnostic build only (make check-exec; not in include/dcol.h): DPP reads from an
+// inactive source lane counted over every kernel launched so far (tools/check_exec.py)
+int dcol_debug_exec_violations(uint64_t* out, int32_t reset) {
+    if (!out) return fail(DCOL_ERR_ARG, "dcol_debug_exec_violations: NULL out");
+    (void)hipDeviceSynchronize();
+    uint64_t total = 0;
+#define DCOL_EXEC_SUM(tag) total += exec_violations_##tag(reset != 0);
+    DCOL_EXEC_TAGS(DCOL_EXEC_SUM)
+#undef DCOL_EXEC_SUM
+    *out = total;
+    return DCOL_SUCCESS;
+}
+#endif
+
 int dcol_prox_batch_host(const dcol_table* tc, int64_t B, const int32_t* s1, const int32_t* s2, const double* pose1,
                          const double* pose2, double tol, int32_t max_iter, int32_t flags, double* alpha,
                          double* contact, double* grad, int32_t* iters, int32_t* status) {
@@ -622,9 +691,8 @@ int dcol_prox_batch_host(const dcol_table* tc, int64_t B, const int32_t* s1, con
     std::lock_guard<std::mutex> lk(t->mu);
     dcol_plan p;   // transient, device arrays are views into the table's staging buffer
     std::vector<int32_t> perm;
-    int rc = bucket_pairs(t, B, s1, s2, &p, perm, (flags & DCOL_CASE4) != 0);
+    int rc = bucket_and_fuse(t, B, s1, s2, &p, perm, (flags & DCOL_CASE4) != 0, true);
     if (rc != DCOL_SUCCESS) return rc;
-    plan_fuse(t, &p, true);
     rc = ensure_fanout(t, &p);
     if (rc != DCOL_SUCCESS) return rc;
     DeviceGuard g(t->device);

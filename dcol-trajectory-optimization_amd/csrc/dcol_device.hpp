@@ -106,7 +106,11 @@ struct DevShape {
     int32_t soc_kind;  // SOC_NONE / SOC_BALL / SOC_CONE
     int32_t n_extra;   // extra primal columns (capsule/cylinder 1, polygon 2)
     int32_t plain;     // r_off == 0 and Q_off == I (make_frame skips the offset products)
-    int32_t pad1, pad2;
+    int32_t n_p;       // orthant rows of the pose form [Qe a, g3, 0..] (polytope faces, cone base,
+                       // cylinder caps); the other n_ort - n_p rows have the extra-column form
+                       // [0 0 0, g3, ex] (capsule / cylinder segment rows, polygon edges).  In the
+                       // row pool the extra-column rows come first, then the pose rows.
+    int32_t pad2;
     double R;          // ball SOC radius (sphere/capsule/cylinder/polygon)
     double cone_c;     // cone SOC row 0, column 3: -(tan(beta) * 3 * H / 4)
     double tanb;       // cone: tan(beta)  (E = diag(tanb, 1, 1))
@@ -428,12 +432,40 @@ DCOL_HD double soc_ls_inv(const double* y, const double* d, double isn, double r
 // value, so the replicated scalar part of the method (Cholesky, mu, sigma, step) takes
 // identical decisions in every lane of the pair.
 #if defined(__HIP_DEVICE_COMPILE__)
+#ifdef DCOL_CHECK_EXEC
+// Diagnostic build (make check-exec, lib_check/): every DPP read whose source lane is
+// inactive is counted -- the only way a reduction could read a register the program never
+// wrote ("Codegen invariance").  A counter, not a trap: a trapping
+// kernel can take the whole GPU down.
+// one counter per translation unit (no relocatable device code): dcol_launch.hpp
+// DCOL_EXEC_READER reads it back
+static __device__ unsigned long long dcol_exec_violations;
+template <int CTRL>
+__device__ __forceinline__ void dpp_check() {
+    const unsigned lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    unsigned src;
+    if (CTRL == 0xB1) src = lane ^ 1u;
+    else if (CTRL == 0x4E) src = lane ^ 2u;
+    else if (CTRL == 0x141) src = (lane & ~7u) | (7u - (lane & 7u));
+    else src = (lane & ~15u) | (15u - (lane & 15u));
+    const unsigned long long exec = __builtin_amdgcn_read_exec();
+    if (!((exec >> src) & 1ull)) atomicAdd(&dcol_exec_violations, 1ull);
+}
+#endif
+// bound_ctrl = true: a lane whose source lane is out of range or disabled reads 0 instead of
+// keeping the destination register's previous (undefined) content, so no schedule can feed
+// an unwritten register into a sum.  Every reduction's group is all-active (a pair's lanes
+// take identical branches), which the DCOL_CHECK_EXEC build verifies, so the results are the
+// same bits either way.
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
+#ifdef DCOL_CHECK_EXEC
+    dpp_check<CTRL>();
+#endif
     const long long b = __double_as_longlong(v);
     int lo = (int)(b & 0xffffffffLL), hi = (int)(b >> 32);
-    lo = __builtin_amdgcn_mov_dpp(lo, CTRL, 0xF, 0xF, false);
-    hi = __builtin_amdgcn_mov_dpp(hi, CTRL, 0xF, 0xF, false);
+    lo = __builtin_amdgcn_mov_dpp(lo, CTRL, 0xF, 0xF, true);
+    hi = __builtin_amdgcn_mov_dpp(hi, CTRL, 0xF, 0xF, true);
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 #define DCOL_XOR1(v) dpp_d<0xB1>(v)   // quad_perm [1,0,3,2]
@@ -543,11 +575,27 @@ struct Grp<4> {
 // held -- scaled by sv = 1 (real block) / 0 (inert slot) -- and every product with the
 // block is written out with its zeros dropped (same nonzero terms in the same order as the
 // dense rows).  Frees 4N doubles of registers per SOC slot.
-template <int N, int NSOC, int OMAX, int LPP, bool BALL = false, bool CONE = false>
+//
+// Row partition (OE > 0, "PART" kernels; N = 5 / 6 pairs of combine cases 1-3, where exactly
+// one primitive has extra columns): every orthant row is either a pose row [Qe a, g3, 0..]
+// (polytope faces, the cone base, cylinder caps) or an extra-column row [0 0 0, g3, ex]
+// (capsule / cylinder segment rows, polygon edges), problem_matrices.py:4-120, :181-209.
+// The lane's first PL = (OMAX - OE) / LPP slots hold pose rows (both primitives', prim 1's
+// first), the last EL = OE / LPP slots the extra-column rows, so each slot's column pattern
+// is known at compile time and every product skips the structural zeros: a row's normal-
+// matrix update is 10 (pose) or 6 (extra) FMAs instead of 21 for N = 6, its G'v / G v terms
+// 4 or 3 instead of 6, and it holds 4 or 3 doubles of G instead of 6.  The rows' reference
+// order within a pair changes, i.e. the lane sums add the same terms in another order
+// (rounding level); parity is pinned by iteration-count equality on every golden vector.
+template <int N, int NSOC, int OMAX, int LPP, bool BALL = false, bool CONE = false, int OE = 0>
 struct Solver {
     static_assert(OMAX % LPP == 0, "OMAX must be a multiple of LPP");
     static_assert(!(BALL && CONE) && (!CONE || N == 4), "CONE: cone-only SOC blocks of N = 4 pairs");
+    static_assert(OE % LPP == 0 && OE <= OMAX && (OE == 0 || (N == 5 || N == 6)), "PART: N = 5 / 6, OE % LPP == 0");
+    static constexpr bool PART = OE > 0;
     static constexpr int OR = OMAX / LPP;              // orthant slots per lane
+    static constexpr int EL = OE / LPP;                // PART: extra-column slots per lane (the last EL)
+    static constexpr int PL = OR - EL;                 // PART: pose slots per lane (the first PL)
     static constexpr int SS = (NSOC + LPP - 1) / LPP;  // SOC slots per lane
     static constexpr int SD = CONE ? 3 : 4;            // rows per SOC slot (cones unpadded in CONE)
     static constexpr int M = OR + SD * SS;             // lane-local rows
@@ -564,6 +612,7 @@ struct Solver {
     double x[N];
     double vimp[N];            // implicit-gradient mode: H^-1 e3 at the returned iterate
     int q, o1, o, deg;
+    int op1, op, oe;           // PART: pose rows of prim 1 / of the pair, extra-column rows
     int xo2;                   // first extra column of primitive 2 minus 4: S1.n_extra for a
                                // case-4 pair (both primitives have extras; opt-in extension),
                                // else 0 (combine_problem_matrices.py cases 1-3)
@@ -573,7 +622,15 @@ struct Solver {
 #endif
     int soc_owner[SSA];        // primitive (0/1) owning the block in SOC slot b
 
-    DCOL_HD bool vort(int k) const { return k * LPP + q < o; }
+    DCOL_HD bool vort(int k) const {
+        if constexpr (PART) return k < PL ? (k * LPP + q < op) : ((k - PL) * LPP + q < oe);
+        return k * LPP + q < o;
+    }
+    // column j of lane row k can be nonzero (compile-time after unrolling): the PART slots'
+    // column patterns; every column of every other row
+    DCOL_HD static constexpr bool nz(int k, int j) {
+        return !PART || k >= OR || (k < PL ? j < 4 : j >= 3);
+    }
     // column offset of a primitive's extra columns (static 0 unless N >= 6 can be case 4)
     DCOL_HD int xoff(bool p2) const { return (N >= 6 && p2) ? xo2 : 0; }
     // value of column j >= 4 of a row whose primitive puts (e0, e1) at columns 4+off, 5+off
@@ -581,7 +638,7 @@ struct Solver {
         const int t = j - 4 - off;
         return t == 0 ? e0 : (t == 1 ? e1 : 0.0);
     }
-    DCOL_HD bool vrow(int k) const { return k < OR ? vort(k) : vs[(k - OR) / 4]; }
+    DCOL_HD bool vrow(int k) const { return k < OR ? vort(k) : vs[(k - OR) / SD]; }
 
     // -------- assembly (problem_matrices.py + combine_problem_matrices.py) --------------
     // One orthant slot: row i = k * LPP + q of primitive p2 (frame F) -> G[k], h in r[k].
@@ -598,8 +655,22 @@ struct Solver {
         G[k][0] = u0; G[k][1] = u1; G[k][2] = u2; G[k][3] = g3;
         const int off = xoff(p2);
 #pragma unroll
-        for (int j = 4; j < N; ++j) G[k][j] = excol(j, off, e0, e1);
+        for (int j = 4; j < N; ++j)
+            if (nz(k, j)) G[k][j] = excol(j, off, e0, e1);
         r[k] = u0 * F.re[0] + u1 * F.re[1] + u2 * F.re[2];
+    }
+    // PART: one extra-column slot (pose-independent row [0 0 0, g3, ex], h = 0)
+    DCOL_HD void ext_row(const double* __restrict__ rows, int k, bool v, int ri) {
+        double g3 = 0, e0 = 0, e1 = 0;
+        if (v) {
+            const double2* rw = reinterpret_cast<const double2*>(rows + 8 * (int64_t)ri);
+            const double2 q1 = rw[1], q2 = rw[2];
+            g3 = q1.y; e0 = q2.x; e1 = q2.y;
+        }
+        G[k][3] = g3;
+#pragma unroll
+        for (int j = 4; j < N; ++j) G[k][j] = excol(j, 0, e0, e1);
+        r[k] = 0.0;
     }
     // leaves h in r[] (init turns it into G x_hat - h)
     DCOL_HD void assemble(const KArgs& A, const DevShape& S1, const DevShape& S2, const Frame& F1, const Frame& F2) {
@@ -608,17 +679,44 @@ struct Solver {
         xo2 = (S1.n_extra > 0 && S2.n_extra > 0) ? S1.n_extra : 0;
         deg = o + NSOC;                                   // quirk Q7
         const double* __restrict__ rows = reinterpret_cast<const double*>(A.rows);
+        if constexpr (PART) {
+            // pose rows of prim 1 then prim 2 in the pose slots (each primitive's pose rows
+            // follow its extra-column rows in the pool); the extra-column rows of the one
+            // primitive that has them in the extra slots
+            op1 = S1.n_p;
+            op = op1 + S2.n_p;
+            oe = o - op;
+            const int eb = S2.n_extra > 0 ? S2.row_off : S1.row_off;
 #pragma unroll
-        for (int k = 0; k < OR; ++k) {
-            const int i = k * LPP + q;
-            const bool v = i < o;
-            const bool p2 = i >= o1;
-            Frame F;   // element-wise select of the row's frame
+            for (int k = 0; k < PL; ++k) {
+                const int i = k * LPP + q;
+                const bool p2 = i >= op1;
+                Frame F;
 #pragma unroll
-            for (int c = 0; c < 9; ++c) F.Qe[c] = p2 ? F2.Qe[c] : F1.Qe[c];
+                for (int c = 0; c < 9; ++c) F.Qe[c] = p2 ? F2.Qe[c] : F1.Qe[c];
 #pragma unroll
-            for (int c = 0; c < 3; ++c) F.re[c] = p2 ? F2.re[c] : F1.re[c];
-            orth_row(rows, k, v, p2, p2 ? (S2.row_off + (i - o1)) : (S1.row_off + i), F);
+                for (int c = 0; c < 3; ++c) F.re[c] = p2 ? F2.re[c] : F1.re[c];
+                const int ri = p2 ? (S2.row_off + (S2.n_ort - S2.n_p) + (i - op1)) : (S1.row_off + (S1.n_ort - S1.n_p) + i);
+                orth_row(rows, k, i < op, p2, ri, F);
+            }
+#pragma unroll
+            for (int k = PL; k < OR; ++k) {
+                const int i = (k - PL) * LPP + q;
+                ext_row(rows, k, i < oe, eb + i);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < OR; ++k) {
+                const int i = k * LPP + q;
+                const bool v = i < o;
+                const bool p2 = i >= o1;
+                Frame F;   // element-wise select of the row's frame
+#pragma unroll
+                for (int c = 0; c < 9; ++c) F.Qe[c] = p2 ? F2.Qe[c] : F1.Qe[c];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) F.re[c] = p2 ? F2.re[c] : F1.re[c];
+                orth_row(rows, k, v, p2, p2 ? (S2.row_off + (i - o1)) : (S1.row_off + i), F);
+            }
         }
         // global SOC block 0 = first primitive with a SOC, block 1 = prim 2 when both have one
         const int own0 = S1.soc_kind != SOC_NONE ? 0 : 1;
@@ -726,6 +824,14 @@ struct Solver {
             if (k >= OR) return ball_row(k, v);
         if constexpr (CONE)
             if (k >= OR) return cone_row(k, v);
+        if constexpr (PART)
+            if (k < OR) {   // the slot's structural nonzeros only
+                const int j0 = k < PL ? 0 : 3, j1 = k < PL ? 4 : N;
+                double acc = G[k][j0] * v[j0];
+#pragma unroll
+                for (int j = j0 + 1; j < j1; ++j) acc += G[k][j] * v[j];
+                return acc;
+            }
         double acc = G[k][0] * v[0];
 #pragma unroll
         for (int j = 1; j < N; ++j) acc += G[k][j] * v[j];
@@ -919,9 +1025,11 @@ struct Solver {
         for (int k = 0; k < MG; ++k) {
 #pragma unroll
             for (int j = 0; j < N; ++j) {
+                if (!nz(k, j)) continue;
                 gth[j] += G[k][j] * r[k];          // r holds h here
 #pragma unroll
-                for (int c = j; c < N; ++c) H[j][c] += G[k][j] * G[k][c];
+                for (int c = j; c < N; ++c)
+                    if (nz(k, c)) H[j][c] += G[k][j] * G[k][c];
             }
         }
         if constexpr (BALL) {                      // the ball rows' products, zeros dropped
@@ -1069,11 +1177,13 @@ struct Solver {
                 const double d = zk * ilv(k, isz);        // W^-2 = z / s on the orthant
                 double g[N];
 #pragma unroll
-                for (int j = 0; j < N; ++j) g[j] = G[k][j] * d;
+                for (int j = 0; j < N; ++j)
+                    if (nz(k, j)) g[j] = G[k][j] * d;
 #pragma unroll
                 for (int j = 0; j < N; ++j)
 #pragma unroll
-                    for (int c = j; c < N; ++c) Hm[j][c] += g[j] * G[k][c];
+                    for (int c = j; c < N; ++c)
+                        if (nz(k, j) && nz(k, c)) Hm[j][c] += g[j] * G[k][c];
             }
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
@@ -1213,7 +1323,8 @@ struct Solver {
             // normal matrix (dd)
             const double t = !cp ? -((z[k] * ilv(k, isz)) * (s[k] + r[k])) : -orth_num(k, cp, smu, s[k] + r[k]) * ilv(k, isz);
 #pragma unroll
-            for (int j = 0; j < N; ++j) rhs[j] += G[k][j] * t;
+            for (int j = 0; j < N; ++j)
+                if (nz(k, j)) rhs[j] += G[k][j] * t;
         }
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
@@ -1321,7 +1432,14 @@ struct Solver {
     }
 
     // -------- gradient helpers ---------------------------------------------------------
+    // orthant slot k holds a row of primitive prim that enters the pose aggregate (PART: the
+    // pose slots; the extra-column rows have no pose columns)
     DCOL_HD bool owns_row(int k, int prim) const {
+        if constexpr (PART) {
+            if (k >= PL) return false;
+            const int i = k * LPP + q;
+            return prim == 0 ? (i < op1) : (i >= op1 && i < op);
+        }
         const int i = k * LPP + q;
         return prim == 0 ? (i < o1) : (i >= o1 && i < o);
     }
@@ -1348,6 +1466,7 @@ struct Solver {
         g.kind = S.soc_kind;
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
+            if (PART && k >= PL) continue;   // extra-column rows: G[k][0:3] = 0
             const double zk = owns_row(k, prim) ? (wt ? wt[k] : z[k]) : 0.0;
 #pragma unroll
             for (int c = 0; c < 3; ++c) g.u[c] = fma(zk, G[k][c], g.u[c]);
@@ -1510,11 +1629,13 @@ struct Solver {
             dd[k] = z[k] * (z[k] * rsz);                      // W^-2 = z / s
             double g[N];
 #pragma unroll
-            for (int j = 0; j < N; ++j) g[j] = G[k][j] * dd[k];
+            for (int j = 0; j < N; ++j)
+                if (nz(k, j)) g[j] = G[k][j] * dd[k];
 #pragma unroll
             for (int j = 0; j < N; ++j)
 #pragma unroll
-                for (int c = j; c < N; ++c) Hm[j][c] += g[j] * G[k][c];
+                for (int c = j; c < N; ++c)
+                    if (nz(k, j) && nz(k, c)) Hm[j][c] += g[j] * G[k][c];
         }
         SocNT W[SSA];
 #pragma unroll
@@ -1609,7 +1730,7 @@ DCOL_HD void launder(P& p) {
 // FULL: every pair of the launch has o == OMAX (no padding rows); BALL: every SOC block of
 // the launch is a ball block (Solver).  The host picks the variant per launch
 // (dcol_capi.cpp: bucket_pairs).
-template <int N, int NSOC, int OMAX, int LPP, bool FULL = false, bool BALL = false, bool CONE = false>
+template <int N, int NSOC, int OMAX, int LPP, bool FULL = false, bool BALL = false, bool CONE = false, int OE = 0>
 DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
     DCOL_STAMP(A, pi, q, 0);
     const int64_t B = A.B;
@@ -1627,7 +1748,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
     make_frame(S2, th2, F2);
     DCOL_STAMP(A, pi, q, 1);
 
-    Solver<N, NSOC, OMAX, LPP, BALL, CONE> P;
+    Solver<N, NSOC, OMAX, LPP, BALL, CONE, OE> P;
     P.q = q;
 #ifdef DCOL_STAMPS
     P.dbg = (q == 0) ? A.stamps + 16 * pi + 8 : nullptr;
@@ -1668,7 +1789,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
             // lane differentiates one primitive: lane q takes primitive q & 1, so a 2+-lane
             // group does the two 6-coordinate gradients side by side instead of both in
             // every lane (a 1-lane group does both in turn)
-            using Agg = typename Solver<N, NSOC, OMAX, LPP, BALL, CONE>::LagAgg;
+            using Agg = typename Solver<N, NSOC, OMAX, LPP, BALL, CONE, OE>::LagAgg;
             const Agg ag0 = P.lag_aggregate(T1, 0);
             const Agg ag1 = P.lag_aggregate(T2, 1);
             // implicit mode: weights a = -W^-2 G v at this iterate, aggregated like z
@@ -1676,7 +1797,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
             Agg agA0 = ag0, agA1 = ag1;
             bool imp_ok = false;
             if (imp) {
-                double wts[Solver<N, NSOC, OMAX, LPP, BALL, CONE>::M];
+                double wts[Solver<N, NSOC, OMAX, LPP, BALL, CONE, OE>::M];
                 imp_ok = P.implicit_weights(wts);
                 agA0 = P.lag_aggregate(T1, 0, wts);
                 agA1 = P.lag_aggregate(T2, 1, wts);
@@ -1751,14 +1872,15 @@ constexpr int kSolveBlock = DCOL_BLOCK;
 static_assert(kSolveBlock % 64 == 0, "one or more whole waves per workgroup");
 
 // FL: variant flags, bit 0 FULL, bit 1 BALL, bit 2 CONE (variants.py)
-template <int N, int NSOC, int OMAX, int LPP, int WPS, int FL>
+// OE > 0: the row-partitioned (PART) copy with OE extra-column row slots (Solver)
+template <int N, int NSOC, int OMAX, int LPP, int WPS, int FL, int OE = 0>
 __global__ void __launch_bounds__(kSolveBlock, WPS) prox_kernel(KArgs A) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t slot = t / LPP;
     const int q = (int)(t % LPP);
     if (slot >= A.n) return;
     const int64_t pi = A.perm ? (int64_t)A.perm[A.slot0 + slot] : (A.slot0 + slot);
-    solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0>(A, pi, q);
+    solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0, OE>(A, pi, q);
 }
 
 }  // namespace dcol

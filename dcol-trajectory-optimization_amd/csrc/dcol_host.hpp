@@ -2,6 +2,7 @@
 // C-ABI (dcol_capi.cpp) and the test-only x86 emulator (tests/emul).
 #pragma once
 #include <algorithm>
+#include <cstdint>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -108,6 +109,7 @@ inline int digest_shape(const dcol_shape_desc& d, int32_t idx, DevShape& S, std:
             if (d.nh < 1 || !d.A || !d.b) return fail(DCOL_ERR_ARG, "shape " + std::to_string(idx) + ": polytope needs nh >= 1, A, b");
             for (int j = 0; j < d.nh; ++j) add(d.A[3 * j], d.A[3 * j + 1], d.A[3 * j + 2], -d.b[j], 0, 0);
             S.n_ort = d.nh;
+            S.n_p = d.nh;
             S.soc_kind = SOC_NONE;
             break;
         case DCOL_SPHERE:     // SOC only   (:151-178)
@@ -119,6 +121,7 @@ inline int digest_shape(const dcol_shape_desc& d, int32_t idx, DevShape& S, std:
             const double tb = std::tan(d.beta);
             add(1.0, 0.0, 0.0, -d.H / 4, 0, 0);
             S.n_ort = 1;
+            S.n_p = 1;
             S.soc_kind = SOC_CONE;
             S.tanb = tb;
             S.cone_c = -(tb * 3 * d.H / 4);
@@ -138,6 +141,7 @@ inline int digest_shape(const dcol_shape_desc& d, int32_t idx, DevShape& S, std:
             add(-1.0, 0, 0, -d.L / 2, 0, 0);
             add(1.0, 0, 0, -d.L / 2, 0, 0);
             S.n_ort = 4;
+            S.n_p = 2;        // the two caps (extra-column rows first, as n_p requires)
             S.soc_kind = SOC_BALL;
             S.R = d.R;
             S.n_extra = 1;
@@ -159,10 +163,61 @@ inline int digest_shape(const dcol_shape_desc& d, int32_t idx, DevShape& S, std:
 struct PairClass {
     int32_t status;   // OK / UNSUPPORTED / TOO_LARGE
     int N, nsoc, o, omax, lpp;
+    int oe = 0;       // row-partitioned bucket: extra-row slots (0: dense-row kernels)
 };
 
-// case4: DCOL_PLAN_CASE4 extension (both primitives with extra columns: n = 4 + e1 + e2)
-inline PairClass classify(const DevShape& a, const DevShape& b, bool case4 = false) {
+// DCOL_NO_PART=1: no row-partitioned kernels (A/B runs, tests)
+inline bool part_disabled() {
+    static const bool off = std::getenv("DCOL_NO_PART") != nullptr;
+    return off;
+}
+
+// Compiled LPP of a PART bucket: the first listed (throughput choice), DCOL_LPP=<n> if that
+// one is compiled, or with latency = true the largest; 0 if the bucket has none (or not the
+// forced one)
+inline int part_lpp(int N, int nsoc, int omax, int oe, bool latency = false) {
+    static const int forced = [] {
+        const char* e = std::getenv("DCOL_LPP");
+        return e ? std::atoi(e) : 0;
+    }();
+    int first = 0, best = 0, hit = 0;
+#define DCOL_PL(NN, NS, OM, LP, WP, FL, OEE)                   \
+    if (NN == N && NS == nsoc && OM == omax && OEE == oe) {    \
+        if (first == 0) first = LP;                            \
+        if (LP > best) best = LP;                              \
+        if (forced == LP) hit = LP;                            \
+    }
+    DCOL_PART_VARIANTS(DCOL_PL)
+#undef DCOL_PL
+    if (latency) return best;
+    if (forced) return hit;
+    return first;
+}
+
+// Row-partitioned bucket of a pair with op pose rows and oe extra-column rows (N = 5 / 6,
+// one primitive with extra columns): the smallest (omax, oe) holding both, fewest slots
+// first, then fewest extra slots (DCOL_PART_SHAPES is sorted that way per (N, NSOC));
+// false if none fits.
+inline bool part_bucket(int N, int nsoc, int op, int oe, PairClass& c) {
+    bool found = false;
+#define DCOL_PB(NN, NS, OM, OEE)                                                           \
+    if (!found && NN == N && NS == nsoc && OM - OEE >= op && OEE >= oe && OEE > 0) {       \
+        const int l = part_lpp(N, nsoc, OM, OEE);                                          \
+        if (l > 0) {                                                                       \
+            c.omax = OM;                                                                   \
+            c.oe = OEE;                                                                    \
+            c.lpp = l;                                                                     \
+            found = true;                                                                  \
+        }                                                                                  \
+    }
+    DCOL_PART_SHAPES(DCOL_PB)
+#undef DCOL_PB
+    return found;
+}
+
+// case4: DCOL_PLAN_CASE4 extension (both primitives with extra columns: n = 4 + e1 + e2);
+// part: row-partitioned buckets allowed (DCOL_NO_PART unset)
+inline PairClass classify(const DevShape& a, const DevShape& b, bool case4 = false, bool part = !part_disabled()) {
     PairClass c{DCOL_OK, 4, 0, 0, 0, 0};
     if (a.n_extra > 0 && b.n_extra > 0 && !case4) {   // combine_problem_matrices.py:58-67 (case 4)
         c.status = DCOL_UNSUPPORTED;
@@ -171,6 +226,10 @@ inline PairClass classify(const DevShape& a, const DevShape& b, bool case4 = fal
     c.N = 4 + a.n_extra + b.n_extra;
     c.nsoc = (a.soc_kind != SOC_NONE) + (b.soc_kind != SOC_NONE);
     c.o = a.n_ort + b.n_ort;
+    if ((a.n_extra > 0) != (b.n_extra > 0) && part) {   // cases 1-3 with extra columns
+        const int op = a.n_p + b.n_p;
+        if (part_bucket(c.N, c.nsoc, op, c.o - op, c)) return c;
+    }
     auto it = buckets().find({c.N, c.nsoc});
     if (it == buckets().end()) {
         c.status = DCOL_TOO_LARGE;

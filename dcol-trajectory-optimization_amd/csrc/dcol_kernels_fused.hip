@@ -13,6 +13,15 @@
 #include "dcol_launch.hpp"
 #include "dcol_variants.inc"
 
+// Development builds (make dev): no cases -- plans launch per bucket (fan-out), and this
+// unit, whose compile time is the sum of its ~100 solver copies, builds in seconds.
+#ifdef DCOL_NO_FUSED_CASES
+#undef DCOL_FUSED_VARIANTS
+#define DCOL_FUSED_VARIANTS(X)
+#undef DCOL_FUSED_PART_VARIANTS
+#define DCOL_FUSED_PART_VARIANTS(X)
+#endif
+
 namespace dcol {
 
 __global__ void __launch_bounds__(kSolveBlock, 1) prox_fused_kernel(KArgs A, const FusedSeg* __restrict__ segs,
@@ -25,13 +34,19 @@ __global__ void __launch_bounds__(kSolveBlock, 1) prox_fused_kernel(KArgs A, con
     const int q = (int)(t % S.lpp);
     if (slot >= S.n) return;
     const int64_t pi = A.perm ? (int64_t)A.perm[S.slot0 + slot] : (S.slot0 + slot);
-    switch (S.vid) {
+    switch (S.vid) {   // NOLINT (empty in development builds)
 #define DCOL_FCASE(ID, NN, NS, OM, LP, FL)                  \
     case ID:                                                \
         solve_one<NN, NS, OM, LP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0>(A, pi, q); \
         break;
         DCOL_FUSED_VARIANTS(DCOL_FCASE)
 #undef DCOL_FCASE
+#define DCOL_FPCASE(ID, NN, NS, OM, LP, FL, OEE)           \
+    case ID:                                                \
+        solve_one<NN, NS, OM, LP, (FL & 1) != 0, (FL & 2) != 0, false, OEE>(A, pi, q); \
+        break;
+        DCOL_FUSED_PART_VARIANTS(DCOL_FPCASE)
+#undef DCOL_FPCASE
         default:
             break;
     }
@@ -40,7 +55,17 @@ __global__ void __launch_bounds__(kSolveBlock, 1) prox_fused_kernel(KArgs A, con
 // (a bucket whose pairs all fill OMAX takes the padding-free case if there is one, a bucket
 // of ball-SOC or cone-SOC pairs the structured case, else the plain one -- as the
 // per-variant launchers do)
-int fused_vid(int N, int nsoc, int omax, int lpp, int flags) {
+int fused_vid(int N, int nsoc, int omax, int lpp, int flags, int oe) {
+    if (oe > 0) {   // row-partitioned bucket: FULL|BALL, BALL, FULL, dense
+        for (const int want : {(int)(LF_FULL | LF_BALL), (int)LF_BALL, (int)LF_FULL, 0}) {
+            if ((want & flags) != want) continue;
+#define DCOL_FPID(ID, NN, NS, OM, LP, FL, OEE) \
+    if (NN == N && NS == nsoc && OM == omax && OEE == oe && LP == lpp && FL == want) return ID;
+            DCOL_FUSED_PART_VARIANTS(DCOL_FPID)
+#undef DCOL_FPID
+        }
+        return -1;
+    }
     for (const int want : {(int)LF_FULL, (int)LF_BALL, (int)LF_CONE, 0}) {
         if ((want & flags) != want) continue;
 #define DCOL_FID(ID, NN, NS, OM, LP, FL) \
@@ -56,5 +81,7 @@ hipError_t launch_fused(const KArgs& args, const FusedSeg* d_segs, int nseg, int
     hipLaunchKernelGGL(prox_fused_kernel, dim3((unsigned)blocks), dim3(kSolveBlock), 0, stream, args, d_segs, nseg);
     return hipGetLastError();
 }
+
+DCOL_EXEC_READER(fused)
 
 }  // namespace dcol

@@ -1,0 +1,6 @@
+// Row-partitioned kernels, N = 6, NSOC = 2 (dcol_kernels_part.inc).
+#define DCOL_TU_N 6
+#define DCOL_TU_NS 2
+#define DCOL_TU_TAG p62
+#define DCOL_TU_FN launch_part_n6s2
+#include "dcol_kernels_part.inc"

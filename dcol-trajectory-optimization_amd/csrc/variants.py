@@ -43,6 +43,18 @@ Generates dcol_variants.inc (FL = variant flags: bit 0 FULL, bit 1 BALL, bit 2 C
   DCOL_CONE_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, 4) for the structured-cone copies
   DCOL_SHAPES(X)    X(N, NSOC, OMAX) once per shape (used by the test emulator)
   DCOL_FUSED_VARIANTS(X)  X(ID, N, NSOC, OMAX, LPP, FL) the cases of the fused kernel
+  DCOL_PART_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, FL, OE) the row-partitioned copies
+  DCOL_PART_SHAPES(X)    X(N, NSOC, OMAX, OE) once per PART bucket (host bucketing, emulator)
+  DCOL_FUSED_PART_VARIANTS(X)  X(ID, N, NSOC, OMAX, LPP, FL, OE) the PART cases of the fused kernel
+
+PART variants (row partition, dcol_device.hpp Solver<..., OE>): N = 5 / 6 pairs of combine
+cases 1-3 (one primitive with extra columns) whose pose rows (polytope faces, cone base,
+cylinder caps) and extra-column rows (capsule / cylinder segment rows, polygon edges) fit a
+bucket (OMAX, OE): OMAX - OE pose-row slots and OE extra-row slots, each slot's column
+pattern fixed at compile time.  A pair takes the smallest bucket that holds both counts
+(fewest slots, then fewest extra slots); pairs that fit none (many-faced polytopes /
+polygons, case 4) stay on the dense-row kernels.  Flavours: BALL (every SOC block a ball:
+x polytope, x sphere) or dense SOC rows (x cone), each with its padding-free FULL copy.
 """
 import os
 
@@ -133,6 +145,49 @@ def configs_fl(n, nsoc, omax, fl):
     return CONFIG_FL.get((n, nsoc, omax, fl), configs(n, nsoc, omax))
 
 
+# PART buckets: (N, NSOC) -> {(OMAX, OE): [(LPP, WPS), ...]} (first = throughput choice)
+PART = {
+    # x polytope: one lane per pair (the SOC block would otherwise idle the group's other lane;
+    # measured 200k pairs: capsule x box 8.1e8 at LPP 2 -> 9.5e8, cylinder x box 6.6 -> 7.1e8)
+    (5, 1): {(8, 2): [(1, 1), (2, 1)], (10, 2): [(1, 1), (2, 1)], (14, 2): [(2, 1)], (18, 2): [(2, 1)]},
+    # x sphere / cone: both lanes own a SOC block (capsule x sphere 11.2e8 at LPP 2, 9.1e8 at 1)
+    (5, 2): {(2, 2): [(2, 1), (1, 1)], (4, 2): [(2, 1), (1, 1)], (6, 2): [(2, 1)]},
+    (6, 1): {(9, 3): [(1, 1)], (10, 4): [(1, 1), (2, 1)], (11, 5): [(1, 1)], (12, 6): [(1, 1), (2, 1)],
+             (14, 8): [(2, 1)]},
+    # pentagon x sphere 7.6e8 at LPP 2 (6, 6) against 6.9e8 at LPP 1 (5, 5)
+    (6, 2): {(4, 4): [(2, 1)], (6, 4): [(2, 1)], (6, 6): [(2, 1), (1, 1)], (8, 6): [(2, 1)], (8, 8): [(2, 1)]},
+}
+
+
+def part_flavours(n, nsoc):
+    """FL list of a PART shape: BALL (+FULL) always; dense SOC rows (+FULL) when the
+    partner can be a cone (NSOC = 2)"""
+    return [3, 2] + ([1, 0] if nsoc == 2 else [])
+
+
+def part_variants():
+    return [(n, s, o, l, w, fl, oe) for (n, s), bl in sorted(PART.items()) for (o, oe), cf in sorted(bl.items())
+            for fl in part_flavours(n, s) for l, w in cf]
+
+
+FUSE_PART_OMAX = 6   # PART buckets in the fused kernel: the small ones (its compile time grows with its cases)
+
+
+def fused_part():
+    """PART cases of the fused kernel: each small ball-SOC bucket of a victim against
+    spheres (the quadrotor hallway's sphere x capsule / cylinder / polygon pairs) in its
+    latency configuration (largest LPP)"""
+    out = []
+    for (n, s), bl in sorted(PART.items()):
+        for (o, oe), cf in sorted(bl.items()):
+            if s != 2 or o > FUSE_PART_OMAX:
+                continue
+            lpp = max(l for l, _ in cf)
+            for fl in (3, 2):
+                out.append((n, s, o, lpp, fl, oe))
+    return out
+
+
 def fused():
     out = []
     for (n, s), os_ in sorted(OMAX.items()):
@@ -170,6 +225,13 @@ def main():
     lines += [f"    X({n}, {s}, {o}) \\" for n, s, o in shapes]
     lines += ["", "#define DCOL_FUSED_VARIANTS(X) \\"]
     lines += [f"    X({i}, {n}, {s}, {o}, {l}, {f}) \\" for i, (n, s, o, l, f) in enumerate(fused())]
+    lines += ["", "#define DCOL_PART_VARIANTS(X) \\"]
+    lines += [f"    X({n}, {s}, {o}, {l}, {w}, {fl}, {oe}) \\" for n, s, o, l, w, fl, oe in part_variants()]
+    lines += ["", "#define DCOL_PART_SHAPES(X) \\"]
+    lines += [f"    X({n}, {s}, {o}, {oe}) \\" for (n, s), bl in sorted(PART.items()) for o, oe in sorted(bl)]
+    lines += ["", "#define DCOL_FUSED_PART_VARIANTS(X) \\"]
+    base = len(fused())
+    lines += [f"    X({base + i}, {n}, {s}, {o}, {l}, {f}, {oe}) \\" for i, (n, s, o, l, f, oe) in enumerate(fused_part())]
     lines.append("")
     out = os.path.join(here, "dcol_variants.inc")
     txt = "\n".join(lines) + "\n"

@@ -47,8 +47,9 @@ extern "C" int dcol_emul_batch(const dcol_shape_desc* shapes, int32_t n, int64_t
     A.status = status;
     const bool no_ball = std::getenv("DCOL_NO_BALL") != nullptr;
     const bool no_cone = std::getenv("DCOL_NO_CONE") != nullptr;
+    const bool part = std::getenv("DCOL_NO_PART") == nullptr;   // read per call (tests toggle it)
     for (int64_t i = 0; i < B; ++i) {
-        PairClass c = classify(sh[s1[i]], sh[s2[i]]);
+        PairClass c = classify(sh[s1[i]], sh[s2[i]], false, part);
         if (c.status != DCOL_OK) {
             alpha[i] = __builtin_nan("");
             iters[i] = 0;
@@ -58,20 +59,19 @@ extern "C" int dcol_emul_batch(const dcol_shape_desc* shapes, int32_t n, int64_t
             continue;
         }
         const bool full = c.o == c.omax;   // both loop specialisations, as the GPU launches pick them
+                                           // (row-partitioned buckets: both slot kinds full)
         // ball-SOC specialisation as the GPU plans pick it (DCOL_NO_BALL: the dense rows)
         const bool ball = c.nsoc > 0 && sh[s1[i]].soc_kind != SOC_CONE && sh[s2[i]].soc_kind != SOC_CONE && !no_ball;
         // structured-cone specialisation (N = 4, every SOC block a cone; DCOL_NO_CONE: dense)
         const bool cone = c.nsoc > 0 && c.N == 4 && sh[s1[i]].soc_kind != SOC_BALL && sh[s2[i]].soc_kind != SOC_BALL &&
                           !no_cone;
         bool done = false;
-        switch (c.N) {
-            case 4: done = emul::solve_n<4>(c, full, ball, cone, A, i); break;
-            case 5: done = emul::solve_n<5>(c, full, ball, cone, A, i); break;
-            case 6: done = emul::solve_n<6>(c, full, ball, cone, A, i); break;
-            case 7: done = emul::solve_n<7>(c, full, ball, cone, A, i); break;
-            case 8: done = emul::solve_n<8>(c, full, ball, cone, A, i); break;
-            default: break;
-        }
+#define EMUL_CASE(NN, NS)                                                                     \
+        if (c.N == NN && c.nsoc == NS)                                                        \
+            done = c.oe > 0 ? emul::solve_part<NN, NS>(c, full, ball, A, i) : emul::solve_n<NN, NS>(c, full, ball, cone, A, i);
+        EMUL_CASE(4, 0) EMUL_CASE(4, 1) EMUL_CASE(4, 2) EMUL_CASE(5, 1) EMUL_CASE(5, 2)
+        EMUL_CASE(6, 1) EMUL_CASE(6, 2) EMUL_CASE(7, 2) EMUL_CASE(8, 2)
+#undef EMUL_CASE
         if (done) continue;
         return fail(DCOL_ERR_ARG, "no variant");
     }

@@ -8,12 +8,13 @@ using namespace dcol;
 using namespace dcol_host;
 
 // Solves pair i of A with the variant the GPU plan would pick for class c (LPP = 1);
-// false if no compiled shape matches.
-template <int X>
+// false if no compiled shape matches.  One instantiation per (N, NSOC) and row form
+// (emul_inst.hip, built once per combination by the Makefile, in parallel).
+template <int X, int XS>
 bool solve_n(const PairClass& c, bool full, bool ball, bool cone, const KArgs& A, int64_t i) {
 #define DCOL_EMUL(NN, NS, OM)                                                      \
-    if constexpr (NN == X) {                                                       \
-        if (c.nsoc == NS && c.omax == OM) {                                        \
+    if constexpr (NN == X && NS == XS) {                                           \
+        if (c.omax == OM) {                                                        \
             if constexpr (NN == 4 && NS == 0) {   /* variants.py FULL shapes */    \
                 if (full) {                                                        \
                     solve_one<NN, NS, OM, 1, true>(A, i, 0);                       \
@@ -42,9 +43,32 @@ bool solve_n(const PairClass& c, bool full, bool ball, bool cone, const KArgs& A
     return false;
 }
 
-extern template bool solve_n<4>(const PairClass&, bool, bool, bool, const KArgs&, int64_t);
-extern template bool solve_n<5>(const PairClass&, bool, bool, bool, const KArgs&, int64_t);
-extern template bool solve_n<6>(const PairClass&, bool, bool, bool, const KArgs&, int64_t);
-extern template bool solve_n<7>(const PairClass&, bool, bool, bool, const KArgs&, int64_t);
-extern template bool solve_n<8>(const PairClass&, bool, bool, bool, const KArgs&, int64_t);
+// row-partitioned buckets (variants.py PART): BALL or dense SOC rows, FULL or padded
+template <int X, int XS>
+bool solve_part(const PairClass& c, bool full, bool ball, const KArgs& A, int64_t i) {
+#define DCOL_EMUL_PART(NN, NS, OM, OEE)                                                        \
+    if constexpr (NN == X && NS == XS) {                                                     \
+        if (c.oe == OEE && c.omax == OM) {                                                   \
+            if (ball) {                                                                      \
+                if (full) solve_one<NN, NS, OM, 1, true, true, false, OEE>(A, i, 0);         \
+                else solve_one<NN, NS, OM, 1, false, true, false, OEE>(A, i, 0);             \
+            } else {                                                                         \
+                if (full) solve_one<NN, NS, OM, 1, true, false, false, OEE>(A, i, 0);        \
+                else solve_one<NN, NS, OM, 1, false, false, false, OEE>(A, i, 0);            \
+            }                                                                                \
+            return true;                                                                     \
+        }                                                                                    \
+    }
+    DCOL_PART_SHAPES(DCOL_EMUL_PART)
+#undef DCOL_EMUL_PART
+    (void)c; (void)full; (void)ball; (void)A; (void)i;
+    return false;
+}
+
+#define EMUL_SOLVE_DECL(X, XS)                                                                              \
+    extern template bool solve_n<X, XS>(const PairClass&, bool, bool, bool, const KArgs&, int64_t);        \
+    extern template bool solve_part<X, XS>(const PairClass&, bool, bool, const KArgs&, int64_t);
+EMUL_SOLVE_DECL(4, 0) EMUL_SOLVE_DECL(4, 1) EMUL_SOLVE_DECL(4, 2) EMUL_SOLVE_DECL(5, 1) EMUL_SOLVE_DECL(5, 2)
+EMUL_SOLVE_DECL(6, 1) EMUL_SOLVE_DECL(6, 2) EMUL_SOLVE_DECL(7, 2) EMUL_SOLVE_DECL(8, 2)
+#undef EMUL_SOLVE_DECL
 }  // namespace emul

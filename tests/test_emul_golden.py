@@ -1,6 +1,7 @@
 """x86 build of the device solver (tests/emul, LPP = 1) against the reference's golden
 vectors -- checks the kernel's arithmetic without a GPU.  Skipped unless the emulator has
-been built (`make -C tests/emul -j6`, ~5 min of hipcc host compilation, one object per N)."""
+been built (`make -C tests/emul -j8`, ~3.5 min of hipcc host compilation, one object per
+(N, NSOC) and row form)."""
 import ctypes
 import os
 
@@ -34,18 +35,24 @@ def emul(d, tol, flags, max_iter=50):
     return al, ct, gr, it, st
 
 
+@pytest.mark.parametrize("orth_rows", ["partitioned", "dense"])
 @pytest.mark.parametrize("soc_rows", ["structured", "dense"])
 @pytest.mark.parametrize("flags", [1 | 4, 2 | 4], ids=["fd", "envelope"])
 @pytest.mark.parametrize("path", [p for p in golden_files() if "tol0" not in p], ids=lambda p: p.split("/")[-1][:-4])
-def test_emulated_kernel_matches_reference(path, flags, soc_rows, monkeypatch):
+def test_emulated_kernel_matches_reference(path, flags, soc_rows, orth_rows, monkeypatch):
     """Both SOC row forms: structured blocks (Solver<..., BALL> for cone-free SOC pairs,
     Solver<..., CONE> for ball-free N = 4 pairs -- what the GPU plans run) and the dense rows
-    (DCOL_NO_BALL, DCOL_NO_CONE)."""
+    (DCOL_NO_BALL, DCOL_NO_CONE); both orthant row forms: the row-partitioned N = 5 / 6
+    buckets (Solver<..., OE>, what the GPU plans run) and the dense rows (DCOL_NO_PART)."""
     for var in ("DCOL_NO_BALL", "DCOL_NO_CONE"):
         if soc_rows == "dense":
             monkeypatch.setenv(var, "1")
         else:
             monkeypatch.delenv(var, raising=False)
+    if orth_rows == "dense":
+        monkeypatch.setenv("DCOL_NO_PART", "1")
+    else:
+        monkeypatch.delenv("DCOL_NO_PART", raising=False)
     d = load_golden(path)
     al, ct, gr, it, st = emul(d, float(d["tol"]), flags)
     np.testing.assert_array_equal(st, d["status"])

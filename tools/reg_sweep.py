@@ -25,17 +25,18 @@ __global__ void __launch_bounds__(64, {w}) kb(KArgs A) {{
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t slot = t / LP; const int q = (int)(t % LP);
     if (slot >= A.n) return;
-    solve_one<N, NS, OM, LP, false, {ball}, {cone}>(A, slot, q);
+    solve_one<N, NS, OM, LP, {full}, {ball}, {cone}, {oe}>(A, slot, q);
 }}
 template __global__ void kb<{n},{s},{o},{l}>(KArgs); }}
 """
 
 
 def run(job, tmp):
-    n, s, o, lpp, w, ball = job
-    fn = os.path.join(tmp, f"k_{n}_{s}_{o}_{lpp}_{w}_{ball}.hip")
+    n, s, o, lpp, w, ball, oe, full = job
+    fn = os.path.join(tmp, f"k_{n}_{s}_{o}_{lpp}_{w}_{ball}_{oe}_{full}.hip")
     open(fn, "w").write(SRC.format(n=n, s=s, o=o, l=lpp, w=w, ball="true" if ball == "ball" else "false",
-                                   cone="true" if ball == "cone" else "false"))
+                                   cone="true" if ball == "cone" else "false", oe=oe,
+                                   full="true" if full else "false"))
     err = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=on", f"-I{CSRC}", "-c",
                           fn, "-o", os.devnull,
                           "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True).stderr
@@ -51,13 +52,21 @@ def main():
     ap.add_argument("--lpp", default="2,4,8")
     ap.add_argument("--ball", action="store_true", help="the ball-SOC copies (Solver<..., BALL>)")
     ap.add_argument("--cone", action="store_true", help="the structured cone copies (Solver<..., CONE>, N = 4)")
+    ap.add_argument("--part", action="store_true",
+                    help="the row-partitioned copies: shapes given as N:NSOC:OMAX:OE (Solver<..., OE>)")
+    ap.add_argument("--full", action="store_true", help="the padding-free loop (solve_one FULL)")
+    ap.add_argument("--waves", default="1,2")
     args = ap.parse_args()
-    shapes = [(n, s, o) for (n, s), os_ in sorted(variants.OMAX.items()) for o in os_]
+    shapes = [(n, s, o, 0) for (n, s), os_ in sorted(variants.OMAX.items()) for o in os_]
+    if args.part and not args.shapes:
+        shapes = [(n, s, o, oe) for (n, s), bl in sorted(variants.PART.items()) for o, oe in bl]
     if args.shapes:
-        shapes = [tuple(int(v) for v in t.split(":")) for t in args.shapes.split(",")]
+        shapes = [tuple(int(v) for v in t.split(":")) + ((0,) if t.count(":") == 2 else ()) for t in args.shapes.split(",")]
     lpps = [int(v) for v in args.lpp.split(",")]
     kind = "ball" if args.ball else ("cone" if args.cone else "")
-    jobs = [(n, s, o, l, w, kind) for n, s, o in shapes for l in lpps if o % l == 0 for w in (1, 2)]
+    waves = [int(v) for v in args.waves.split(",")]
+    jobs = [(n, s, o, l, w, kind, oe, args.full) for n, s, o, oe in shapes for l in lpps
+            if o % l == 0 and oe % l == 0 for w in waves]
     with tempfile.TemporaryDirectory() as tmp, ThreadPoolExecutor(args.j) as ex:
         for job, v, a, sc, oc in ex.map(lambda j: run(j, tmp), jobs):
             print(*job, "vgpr", v, "agpr", a, "scratch", sc, "occ", oc, flush=True)
