@@ -43,6 +43,11 @@ for _p in (PKG, REPO):
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 FP64_VECTOR_PEAK_TFS = 78.6    # MI355X FP64 vector peak (AMD spec)
 BYTES_PER_PAIR = 208           # poses 2x6 f64 + 2 int32 ids in; alpha + 12 grad f64 out
+# The reference itself (proximity_gradient, NumPy, one core) measured in the survey container:
+# random polytope-polytope 1.76-1.93 ms per pair, about 520 pair-solves/s per core (SURVEY.md
+# section 6).  The baselines below are restatements ("port"), not the reference, and run
+# faster per core; the line states the ratio so neither is mistaken for the reference's speed.
+REFERENCE_PER_CORE = 520.0
 
 
 def shape_table(n_shapes=64, seed=0):
@@ -90,7 +95,15 @@ def cpu_baseline(tab, s1, s2, p1, p2, sample, workers):
     return {"value": n / wall, "unit": "pair-solves/s", "cores": len(jobs), "kind": "port",
             "sample": f"{n} of the same synthetic poly-poly pairs, proximity+FD gradient, NumPy oracle "
                       f"(oracle/dcol_oracle.py), {len(jobs)} processes, {cpu_s:.1f} s CPU, {wall:.1f} s wall",
-            "per_core": n / cpu_s}
+            "per_core": n / cpu_s, **calibration(n / cpu_s)}
+
+
+def calibration(per_core):
+    """the port's per-core rate against the reference's own (REFERENCE_PER_CORE)"""
+    return {"reference_per_core": REFERENCE_PER_CORE,
+            "reference_per_core_source": "SURVEY.md section 6: the reference's proximity_gradient on one core, "
+                                         "random polytope-polytope pairs, 1.76-1.93 ms per pair",
+            "port_vs_reference_per_core": per_core / REFERENCE_PER_CORE}
 
 
 def cpu_baseline_c(tab, s1, s2, p1, p2, threads, seconds=3.0):
@@ -110,7 +123,7 @@ def cpu_baseline_c(tab, s1, s2, p1, p2, threads, seconds=3.0):
     return {"value": done / wall, "unit": "pair-solves/s", "cores": threads, "kind": "port",
             "sample": f"{done} solves ({n} distinct synthetic poly-poly pairs), proximity+FD gradient, C oracle "
                       f"(oracle/dcol_oracle.c), OpenMP {threads} threads, {wall:.1f} s wall",
-            "per_core": done / wall / threads}
+            "per_core": done / wall / threads, **calibration(done / wall / threads)}
 
 
 def spawn_ranks(n):
@@ -353,6 +366,7 @@ def main():
     if world == 1 and not args.no_altro:
         line["altro"] = altro_section()
         line["scene_batches"] = scene_batches(local)
+        line["dropin"] = dropin_section()
     if world == 1 and not args.no_cpu:
         workers, host = cpu_share(args.cpu_workers)
         line["cpu_baseline"] = cpu_baseline(tab, s1, s2, p1, p2, args.cpu_sample, workers)
@@ -579,8 +593,9 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
             launch()
             rec[:n, 0] = out["alpha"]
             rec[:n, 1:13] = out["grad"].T
-            rec[:n, 13] = out["status"].to(torch.float64)
-            rec[:n, 14] = out["iters"].to(torch.float64)
+            # (status, iters) as an int32 pair in the last slot (dcol_amd.dist.REC)
+            rec[:n, 13] = ((out["iters"].to(torch.int64) << 32) | (out["status"].to(torch.int64) & 0xFFFFFFFF)).view(
+                torch.float64)
             if dist is not None:
                 dist.all_gather_into_tensor(gathered, rec.to(coll_dev))
             else:
@@ -617,13 +632,27 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
         e1.record(stream)
     torch.cuda.synchronize(dev)
     solve_ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
-    flops_local = mixed_flops(tab, s1[mine], s2[mine], out["iters"].cpu().numpy(), out["status"].cpu().numpy(), args.grad)
+    # the whole step (solve + pack + all-gather) the same way: its excess over the solve is
+    # the communication cost of the step (5-50 % predicted at 8 GPUs)
+    for e0, e1 in ev:
+        e0.record(stream)
+        step()
+        e1.record(stream)
+    torch.cuda.synchronize(dev)
+    step_ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
+    my_iters = out["iters"].cpu().numpy()
+    my_status = out["status"].cpu().numpy()
+    flops_local = mixed_flops(tab, s1[mine], s2[mine], my_iters, my_status, args.grad)
+    # per-rank shard figures (load balance): solve ms, step ms, mean Newton iterations
+    mine_stats = [solve_ms, step_ms, float(my_iters[my_status == 0].mean()) if (my_status == 0).any() else 0.0, float(n)]
     if dist is not None:
-        t = torch.tensor([solve_ms], device=coll_dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        solve_ms_max = float(t[0])
+        t = torch.zeros((world, 4), device=coll_dev, dtype=torch.float64)
+        t[rank] = torch.tensor(mine_stats, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        ranks_stats = t.cpu().numpy()
     else:
-        solve_ms_max = solve_ms
+        ranks_stats = np.array([mine_stats])
+    solve_ms_max = float(ranks_stats[:, 0].max())
     torch.cuda.synchronize(dev)
     allrec = gathered.cpu().numpy().reshape(world, cap, REC)
     if comm is not None:
@@ -634,7 +663,9 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
     full = np.empty((B, REC))
     for r, ix in enumerate(idx):
         full[ix] = allrec[r, :len(ix)]
-    status = full[:, 13].astype(np.int32)
+    from dcol_amd.dist import unpack
+    res_all = unpack(full)
+    status = res_all["status"]
     line = {
         "metric": "PDIP proximity+grad pair-solves/sec", "value": B * steps / elapsed, "unit": "pair-solves/s",
         "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": 1e3 * elapsed / steps,
@@ -642,10 +673,18 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
         "config": {"workload": "synthetic 1M mixed-primitive pairs sharded across GPUs + RCCL all-gather "
                                "(BASELINE.json configs[4])", "pairs_total": B, "pairs_per_gpu": cap,
                    "kinds": "polytope sphere cone capsule cylinder polygon; 27 supported ordered kind pairs",
-                   "gradient": args.grad, "collective": f"{path}: one all-gather of [alpha, grad(12), status, iters]",
+                   "gradient": args.grad, "collective": f"{path}: one all-gather of [alpha, grad(12), (status, iters) int32]",
                    "parallelism": f"dp{world} (class-balanced shards)"},
-        "solve_stats": {"ok_frac": float(np.mean(status == 0)), "iters_mean": float(full[status == 0, 14].mean())},
+        "solve_stats": {"ok_frac": float(np.mean(status == 0)), "iters_mean": float(res_all["iters"][status == 0].mean())},
         "solve_ms_rank0": solve_ms, "solve_ms_max_rank": solve_ms_max,
+        "step_breakdown": {
+            "note": "HIP events on each rank's launch stream, one step at a time (median of 10): solve = the "
+                    "plan run alone; step = solve + pack_records + all-gather; comm = step - solve",
+            "solve_ms_max_rank": solve_ms_max, "step_ms_max_rank": float(ranks_stats[:, 1].max()),
+            "comm_ms_rank0": step_ms - solve_ms, "comm_frac_rank0": (step_ms - solve_ms) / step_ms if step_ms > 0 else None,
+            "record_bytes_per_pair": REC * 8,
+            "per_rank": {"solve_ms": ranks_stats[:, 0].tolist(), "step_ms": ranks_stats[:, 1].tolist(),
+                         "iters_mean": ranks_stats[:, 2].tolist(), "pairs": ranks_stats[:, 3].astype(int).tolist()}},
         "pipeline": {"streams": max(1, len(lanes)),
                      "serial_value": B * steps / elapsed_serial if elapsed_serial else B * steps / elapsed,
                      "serial_ms_per_step": 1e3 * (elapsed_serial or elapsed) / steps},
@@ -694,6 +733,53 @@ def mixed_flops(tab, s1, s2, iters, status, grad="fd"):
             g = GRAD_OPS.get(grad, c["grad_fd"])   # closed-form modes: the poly x poly hand counts
             total += m.sum() * (c["assembly"] + c["pdip_fixed"] + g) + c["pdip_per_iter"] * iters[m].sum()
     return total
+
+
+# The reference's quadrotor ALTRO run (quadrotor.prof): 377,311 PDIP solves,
+# 66,000 of them through proximity_gradient (one solve each), the rest through proximity_mrp
+QUAD_SOLVES, QUAD_GRAD_CALLS = 377_311, 66_000
+
+
+def dropin_section(reps=3):
+    """The drop-in's per-call latency (BASELINE north star: ALTRO.py drops in unchanged):
+    the reference's own calling pattern -- for every knot of the quadrotor's reference
+    trajectory, overwrite P_vic.r / .p, then call proximity_mrp (inequality_constraints_x,
+    cluttered_hallway_quadrotor.py:115-135) or proximity_gradient
+    (inequality_constraints_x_grad, :137-171) once per obstacle -- timed on the host clock,
+    one call at a time.  Best of `reps` sweeps; projected onto the reference's quadrotor run
+    (QUAD_SOLVES solves, QUAD_GRAD_CALLS of them gradient calls)."""
+    from altro import systems
+    from proximity.proximity import proximity_mrp
+    from proximity.proximity_gradient import proximity_gradient
+    params, X, U = systems.initialize("quadrotor")
+    vic, obs = params["P_vic"], params["P_obs"]
+    nx = int(params["nx"])
+    Xr = np.asarray(params["Xref"], dtype=np.float64).reshape(-1, nx)
+    out = {"pattern": f"{len(Xr)} knots x {len(obs)} obstacles of the quadrotor hallway, one call per pair "
+                      "(P_vic.r / .p overwritten per knot)", "calls_per_sweep": len(Xr) * len(obs)}
+    for name, fn in (("proximity_mrp", proximity_mrp), ("proximity_gradient", proximity_gradient)):
+        for o in obs:                     # first call per pair kind: its plan, code objects
+            vic.r, vic.p = np.array(Xr[0, 0:3]), np.array(Xr[0, 6:9])
+            fn(vic, o)
+        best = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            for x in Xr:
+                vic.r = np.array(x[0:3])
+                vic.p = np.array(x[6:9])
+                for o in obs:
+                    fn(vic, o)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        out[name] = {"us_per_call": 1e6 * best / (len(Xr) * len(obs))}
+    t_mrp, t_grad = out["proximity_mrp"]["us_per_call"], out["proximity_gradient"]["us_per_call"]
+    proj = ((QUAD_SOLVES - QUAD_GRAD_CALLS) * t_mrp + QUAD_GRAD_CALLS * t_grad) * 1e-6
+    out["projected_quadrotor_altro"] = {
+        "solves": QUAD_SOLVES, "gradient_calls": QUAD_GRAD_CALLS, "proximity_s": proj,
+        "reference_altro_wall_s": ALTRO_REFERENCE["quadrotor"]["python_s"],
+        "note": "time the unchanged reference ALTRO.py would spend in the drop-in proximity calls on this GPU "
+                "(its own Python around them excluded); the batched driver (altro section) is the fast path"}
+    return out
 
 
 def scene_batches(device):

@@ -117,6 +117,12 @@ struct dcol_table {
     // of the device (device_side_streams), shared by every table
     hipStream_t side[kSideStreams] = {};
     bool side_ready = false;
+    // dcol_prox_pair: one-pair plans per (shape1, shape2), a stream, and device-mapped pinned
+    // staging [pose1 (6) | pose2 (6) | alpha | contact (3) | grad (12) | (iters, status)]
+    std::unordered_map<int64_t, dcol_plan*> pair_plans;
+    hipStream_t pair_stream = nullptr;
+    double* pair_host = nullptr;
+    double* pair_dev = nullptr;
 };
 
 struct Launch {
@@ -244,6 +250,9 @@ int dcol_table_create(const dcol_shape_desc* shapes, int32_t n, int32_t device, 
 int dcol_table_destroy(dcol_table* t) {
     if (!t) return DCOL_SUCCESS;
     DeviceGuard g(t->device);
+    for (auto& kv : t->pair_plans) dcol_plan_destroy(kv.second);
+    if (t->pair_stream) (void)hipStreamDestroy(t->pair_stream);
+    if (t->pair_host) (void)hipHostFree(t->pair_host);
     if (t->d_shapes) (void)hipFree(t->d_shapes);
     if (t->d_rows) (void)hipFree(t->d_rows);
     if (t->stage) (void)hipFree(t->stage);
@@ -665,6 +674,61 @@ int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, 
     return DCOL_SUCCESS;
 }
 
+int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* pose1, const double* pose2, double tol,
+                   int32_t max_iter, int32_t flags, double* alpha, double* contact, double* grad, int32_t* iters,
+                   int32_t* status) {
+    if (!tc || !pose1 || !pose2 || !alpha) return fail(DCOL_ERR_ARG, "dcol_prox_pair: NULL argument");
+    if ((flags & DCOL_CONTACT) && !contact) return fail(DCOL_ERR_ARG, "dcol_prox_pair: DCOL_CONTACT needs contact");
+    if ((flags & DCOL_GRAD_ANY) && !grad) return fail(DCOL_ERR_ARG, "dcol_prox_pair: gradient flag needs grad");
+    if (max_iter < 0) return fail(DCOL_ERR_ARG, "dcol_prox_pair: max_iter < 0");
+    const int32_t ns = (int32_t)tc->shapes.size();
+    if (s1 < 0 || s1 >= ns || s2 < 0 || s2 >= ns) return fail(DCOL_ERR_ARG, "dcol_prox_pair: shape id out of range");
+    dcol_table* t = const_cast<dcol_table*>(tc);
+    std::lock_guard<std::mutex> lk(t->mu);
+    DeviceGuard g(t->device);
+    constexpr int kSlots = 12 + 1 + 3 + 12 + 1;
+    if (!t->pair_host) {
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&t->pair_host), kSlots * sizeof(double),
+                                     hipHostMallocMapped | hipHostMallocPortable);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&t->pair_dev), t->pair_host, 0);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&t->pair_stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            if (t->pair_host) (void)hipHostFree(t->pair_host);
+            t->pair_host = t->pair_dev = nullptr;
+            t->pair_stream = nullptr;
+            return fail(DCOL_ERR_HIP, std::string("dcol_prox_pair staging: ") + hipGetErrorString(e));
+        }
+    }
+    const int64_t key = (int64_t)s1 * ns + s2;
+    const bool c4 = (flags & DCOL_CASE4) != 0;
+    const int64_t ck = c4 ? -1 - key : key;   // case-4 plans apart
+    auto it = t->pair_plans.find(ck);
+    if (it == t->pair_plans.end()) {
+        dcol_plan* p = nullptr;
+        const int rc = dcol_plan_create_ex(t, 1, &s1, &s2, c4 ? DCOL_PLAN_CASE4 : 0, &p);
+        if (rc != DCOL_SUCCESS) return rc;
+        it = t->pair_plans.emplace(ck, p).first;
+    }
+    double* h = t->pair_host;
+    double* d = t->pair_dev;
+    std::memcpy(h, pose1, 6 * sizeof(double));
+    std::memcpy(h + 6, pose2, 6 * sizeof(double));
+    int32_t* hi = reinterpret_cast<int32_t*>(h + 28);
+    int32_t* di = reinterpret_cast<int32_t*>(d + 28);
+    // SoA of one pair = the 6 values in order; the kernel reads / writes the mapped memory
+    int rc = dcol_plan_run(it->second, d, d + 6, tol, max_iter, flags & ~DCOL_CASE4, d + 12, d + 13, d + 16, di, di + 1,
+                           t->pair_stream);
+    if (rc != DCOL_SUCCESS) return rc;
+    const hipError_t e = hipStreamSynchronize(t->pair_stream);
+    if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_prox_pair: ") + hipGetErrorString(e));
+    *alpha = h[12];
+    if (contact && (flags & DCOL_CONTACT)) std::memcpy(contact, h + 13, 3 * sizeof(double));
+    if (grad && (flags & DCOL_GRAD_ANY)) std::memcpy(grad, h + 16, 12 * sizeof(double));
+    if (iters) *iters = hi[0];
+    if (status) *status = hi[1];
+    return DCOL_SUCCESS;
+}
+
 #ifdef DCOL_CHECK_EXEC
 // diagnostic build only (make check-exec; not in include/dcol.h): DPP reads from an
 // inactive source lane counted over every kernel launched so far (tools/check_exec.py)
@@ -816,7 +880,8 @@ struct dcol_comm {
 };
 
 namespace dcol {
-// rec[i] = [alpha, grad(12), status, iters] (dcol_amd/dist.py REC layout); rows >= n NaN.
+// rec[i] = [alpha, grad(12), (int32 status, int32 iters)] (dcol_amd/dist.py REC layout);
+// rows >= n NaN.
 // A block packs kPackRows records: each thread gathers one record's fields from the SoA
 // outputs (coalesced reads) into LDS, then the block streams the contiguous
 // kPackRows * DCOL_REC doubles out with consecutive threads on consecutive addresses
@@ -834,8 +899,9 @@ __global__ void __launch_bounds__(kPackRows) pack_records(int64_t n, int64_t cap
         o[0] = alpha[i];
 #pragma unroll
         for (int c = 0; c < 12; ++c) o[1 + c] = grad ? grad[c * n + i] : nan;
-        o[13] = (double)status[i];
-        o[14] = (double)iters[i];
+        // the int32 pair in one 8-byte slot (status low, iters high: little-endian)
+        o[13] = __longlong_as_double((long long)(((unsigned long long)(unsigned)iters[i] << 32) |
+                                                 (unsigned long long)(unsigned)status[i]));
     } else {
 #pragma unroll
         for (int c = 0; c < DCOL_REC; ++c) o[c] = nan;

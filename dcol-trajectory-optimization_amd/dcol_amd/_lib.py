@@ -22,7 +22,7 @@ GRAD_ANY = GRAD_FD | GRAD_ENVELOPE | GRAD_IMPLICIT
 # enum dcol_plan_options
 PLAN_CASE4, PLAN_NO_FUSE = 1, 2
 SUCCESS, ERR_ARG, ERR_HIP, ERR_NOMEM = 0, -1, -2, -3
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class DcolLibraryError(RuntimeError):
@@ -56,6 +56,8 @@ SIGNATURES = {
                               c_void_p, c_void_p, c_void_p, c_void_p]),
     "dcol_prox_batch_host": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_double,
                                      c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "dcol_prox_pair": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_double, c_int32, c_int32, c_void_p,
+                               c_void_p, c_void_p, c_void_p, c_void_p]),
     "dcol_comm_unique_id": (c_int, [c_void_p]),
     "dcol_comm_create": (c_int, [c_void_p, c_int32, c_int32, c_int32, POINTER(c_void_p)]),
     "dcol_comm_destroy": (c_int, [c_void_p]),

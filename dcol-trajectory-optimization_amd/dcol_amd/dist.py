@@ -16,7 +16,8 @@ from __future__ import annotations
 
 import numpy as np
 
-REC = 15   # packed record per pair: alpha, grad[12], status, iters (float64)
+REC = 14   # packed record per pair: alpha, grad[12] (float64), then (status, iters) as two int32
+           # in the last 8-byte slot (include/dcol.h DCOL_REC)
 
 
 def shard_indices(B: int, rank: int, world: int, cost_key=None) -> np.ndarray:
@@ -38,20 +39,28 @@ def shard_sizes(B: int, world: int, balanced: bool) -> list[int]:
     return [int(bounds[r + 1] - bounds[r]) for r in range(world)]
 
 
+def _ints(rec):
+    """[n, REC] float64 records -> [n, 2] int32 (status, iters) of the last slot"""
+    return np.ascontiguousarray(rec[:, 13]).view(np.int32).reshape(-1, 2)
+
+
 def pack(alpha, grad, status, iters):
-    """Per-pair results -> [n, REC] float64 record (status/iters exact in float64)."""
+    """Per-pair results -> [n, REC] float64 record (status / iters bit-packed, exact)."""
     n = len(alpha)
     rec = np.empty((n, REC), dtype=np.float64)
     rec[:, 0] = alpha
     rec[:, 1:13] = grad if grad is not None else np.nan
-    rec[:, 13] = status
-    rec[:, 14] = iters
+    ints = np.empty((n, 2), dtype=np.int32)
+    ints[:, 0] = status
+    ints[:, 1] = iters
+    rec[:, 13] = ints.view(np.float64).reshape(n)
     return rec
 
 
 def unpack(rec):
+    ints = _ints(rec)
     return {"alpha": rec[:, 0].copy(), "grad": rec[:, 1:13].copy(),
-            "status": rec[:, 13].astype(np.int32), "iters": rec[:, 14].astype(np.int32)}
+            "status": ints[:, 0].copy(), "iters": ints[:, 1].copy()}
 
 
 class ShardedBatch:

@@ -11,9 +11,9 @@ def proximity_mrp(prim1, prim2, pdip_tol=DEFAULT_TOL, verbose=False):
     """-> (alpha: float64, contact_point: ndarray(3)).  Raises like the reference:
     Exception after 50 PDIP iterations, ValueError for unsupported pairs,
     numpy.linalg.LinAlgError for a non-PD normal matrix."""
-    res = default_engine().solve_objects([prim1], [prim2], tol=pdip_tol, grad=None, contact=True)
-    raise_for_status(int(res.status[0]))
-    return res.alpha[0], res.contact[0]
+    alpha, contact, _, _, status = default_engine().solve_pair(prim1, prim2, tol=pdip_tol, grad=None, contact=True)
+    raise_for_status(status)
+    return alpha, contact
 
 
 def proximity_mrp_batch(prims1, prims2, pdip_tol=DEFAULT_TOL):

@@ -10,9 +10,9 @@ from dcol_amd.engine import DEFAULT_TOL, default_engine, raise_for_status
 
 def proximity_gradient(prim1, prim2, pdip_tol=DEFAULT_TOL, verbose=False):
     """-> (alpha: float64, d_alpha_d_state: ndarray(12)).  Raises like the reference."""
-    res = default_engine().solve_objects([prim1], [prim2], tol=pdip_tol, grad="fd", contact=False)
-    raise_for_status(int(res.status[0]))
-    return res.alpha[0], res.grad[0]
+    alpha, _, grad, _, status = default_engine().solve_pair(prim1, prim2, tol=pdip_tol, grad="fd", contact=False)
+    raise_for_status(status)
+    return alpha, grad
 
 
 def proximity_gradient_batch(prims1, prims2, pdip_tol=DEFAULT_TOL, grad="fd"):

@@ -11,8 +11,10 @@
  *     primitives/problem_matrices.py:255-364                     once to HBM)
  *   proximity_mrp(prim1, prim2, pdip_tol) -> (alpha, x[:3])   dcol_plan_run(flags=CONTACT)
  *     proximity/proximity.py:6-54                             dcol_prox_batch_host()
+ *                                                             dcol_prox_pair() (one pair)
  *   proximity_gradient(prim1, prim2, pdip_tol)                dcol_plan_run(flags=GRAD_FD)
  *     -> (alpha, d_alpha/d[r1,p1,r2,p2])                      dcol_prox_batch_host()
+ *                                                             dcol_prox_pair() (one pair)
  *     proximity/proximity_gradient.py:91-138
  *   combine_problem_matrices() + solve_lp_pdip()              inside the device kernel
  *     primitives/combine_problem_matrices.py:3-70,
@@ -35,7 +37,7 @@
 extern "C" {
 #endif
 
-#define DCOL_ABI_VERSION 1
+#define DCOL_ABI_VERSION 2   /* 2: 14-slot multi-GPU record (status / iters as an int32 pair) */
 
 /* Primitive types (misc_primitive_constructor.py:4-88). */
 enum dcol_shape_type {
@@ -161,6 +163,18 @@ int dcol_prox_batch_host(const dcol_table* table, int64_t B, const int32_t* shap
                          double tol, int32_t max_iter, int32_t flags, double* alpha,
                          double* contact, double* grad, int32_t* iters, int32_t* status);
 
+/* The drop-in's per-call form (proximity/proximity.py:6-54, proximity_gradient.py:91-138:
+ * ONE pair per call, which is how the reference's systems call it, per obstacle per knot --
+ * systems/cluttered_hallway_quadrotor.py:131-133, :155).  HOST arguments: pose1/pose2 (6),
+ * contact (3, if DCOL_CONTACT, else may be NULL), grad (12, if a GRAD flag, else may be NULL),
+ * iters / status (may be NULL).  Synchronous.  Latency path: a one-pair plan cached per
+ * (shape1, shape2) in the table, poses and outputs in device-mapped pinned host memory read
+ * and written by the kernel itself (no copy commands), one launch on a stream of the table.
+ * Calls on one table are serialised.                                                      */
+int dcol_prox_pair(const dcol_table* table, int32_t shape1, int32_t shape2, const double* pose1,
+                   const double* pose2, double tol, int32_t max_iter, int32_t flags, double* alpha,
+                   double* contact, double* grad, int32_t* iters, int32_t* status);
+
 /* ---- multi-GPU ------------------------------------------------------
  * One process per GPU.  Pairs are independent, so each rank solves its own shard with its
  * own plan; when one consumer needs the whole batch, dcol_prox_batch_multi_gpu packs the
@@ -168,7 +182,9 @@ int dcol_prox_batch_host(const dcol_table* table, int64_t B, const int32_t* shap
  * use).  Bootstrap: rank 0 calls dcol_comm_unique_id and ships the 128 bytes to the other
  * ranks by the host's own means (the reference's Python: torch.distributed / a file).  */
 #define DCOL_COMM_ID_BYTES 128
-#define DCOL_REC 15 /* packed per-pair record: alpha, grad[12], status, iters (float64) */
+/* packed per-pair record, 14 x 8 B = 112 B: alpha, grad[12] (float64), then status and iters
+ * as two int32 (little-endian: status in the low half) in the last 8-byte slot           */
+#define DCOL_REC 14
 typedef struct dcol_comm dcol_comm;
 int dcol_comm_unique_id(uint8_t id[DCOL_COMM_ID_BYTES]);
 /* Collective over the nranks processes (ncclCommInitRank); `device` = this rank's GPU.   */
@@ -178,7 +194,7 @@ int dcol_comm_destroy(dcol_comm* comm);
 /* Solve this rank's shard (plan over its n pairs; pose1/pose2 SoA [6][n] and the
  * alpha[n] / grad[12][n] (or NULL) / iters[n] / status[n] outputs are device arrays, as
  * dcol_plan_run), pack row i of rec_local[cap][DCOL_REC] = [alpha, grad(12) (NaN without a
- * gradient flag), status, iters] (rows n..cap-1 = NaN), then all-gather every rank's
+ * gradient flag), (int32 status, int32 iters)] (rows n..cap-1 = NaN), then all-gather every rank's
  * rec_local into rec_all[nranks * cap][DCOL_REC] (rank r's rows at r * cap).  Requires
  * n <= cap, the same cap on every rank.  Asynchronous on `stream`; no allocation.       */
 int dcol_prox_batch_multi_gpu(const dcol_plan* plan, dcol_comm* comm, const double* pose1, const double* pose2,
