@@ -129,6 +129,13 @@ struct Launch {
     int kind;       // 0 = solve, 1 = reject
     int N, nsoc, omax, lpp;
     int oe = 0;          // row-partitioned bucket (extra-row slots; 0: dense-row kernels)
+    // suspend / resume pair (DCOL_PLAN_SUSPEND): continuation entries, their buffers
+    bool susp = false;
+    int susp_fields = 0;
+    int64_t susp_cap = 0;
+    int32_t* d_susp_count = nullptr;
+    int32_t* d_susp_pi = nullptr;
+    double* d_susp_state = nullptr;
     bool full = false;   // every pair has o == omax: the padding-free kernel (DCOL_FULL_VARIANTS) if built
     bool ball = false;   // every SOC block is a ball block: the structured kernel (DCOL_BALL_VARIANTS) if built
     bool cone = false;   // every SOC block is a cone block (N = 4): DCOL_CONE_VARIANTS if built
@@ -154,6 +161,7 @@ struct dcol_plan {
     FusedSeg* d_segs = nullptr;
     int64_t fused_blocks = 0;
     bool fused() const { return !segs.empty(); }
+    void* d_susp = nullptr;      // DCOL_PLAN_SUSPEND scratch (one allocation for every such launch)
     ~dcol_plan() {
         if (fork) (void)hipEventDestroy(fork);
         for (hipEvent_t& e : join)
@@ -465,6 +473,53 @@ void assign_lanes(dcol_plan* p) {
 // than one wave per SIMD: every bucket already took its latency configuration) runs as ONE
 // fused launch; p->segs is left empty when it does not qualify (large or single-variant
 // plans, variants outside the fused kernel, DCOL_PLAN_NO_FUSE).
+// DCOL_PLAN_SUSPEND: every large solve bucket with a suspend / resume variant gets its
+// continuation buffers (entries: DCOL_SUSPEND_T per wave, default 4; DCOL_NO_SUSPEND=1
+// disables).  Allocates; returns DCOL_SUCCESS or an error.
+int susp_t_env() {
+    static const int t = [] {
+        const char* e = std::getenv("DCOL_SUSPEND_T");
+        return std::getenv("DCOL_NO_SUSPEND") ? 0 : (e ? std::max(0, std::atoi(e)) : 4);
+    }();
+    return t;
+}
+int susp_min_env() {
+    static const int m = [] {
+        const char* e = std::getenv("DCOL_SUSPEND_MIN");
+        return e ? std::max(0, std::atoi(e)) : 6;
+    }();
+    return m;
+}
+int plan_susp(const dcol_table* t, dcol_plan* p) {
+    const int T = susp_t_env();
+    if (T <= 0 || p->fused()) return DCOL_SUCCESS;
+    size_t bytes = 0;
+    for (Launch& L : p->launches) {
+        int f = 0;
+        if (L.kind != 0 || L.n * L.lpp < 64LL * t->simds || !susp_available(L.N, L.nsoc, L.omax, L.lpp, L.flags(), L.oe, &f))
+            continue;
+        L.susp = true;
+        L.susp_fields = f;
+        L.susp_cap = ((L.n * L.lpp + 63) / 64) * (int64_t)T;
+        bytes += 256 + (size_t)L.susp_cap * (sizeof(int32_t) + sizeof(double) * f);
+    }
+    if (bytes == 0) return DCOL_SUCCESS;
+    DeviceGuard g(t->device);
+    hipError_t e = hipMalloc(&p->d_susp, bytes);
+    if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("suspend scratch: ") + hipGetErrorString(e));
+    char* c = static_cast<char*>(p->d_susp);
+    for (Launch& L : p->launches) {
+        if (!L.susp) continue;
+        L.d_susp_count = reinterpret_cast<int32_t*>(c);
+        c += 256;
+        L.d_susp_state = reinterpret_cast<double*>(c);
+        c += sizeof(double) * L.susp_fields * (size_t)L.susp_cap;
+        L.d_susp_pi = reinterpret_cast<int32_t*>(c);
+        c += sizeof(int32_t) * (size_t)L.susp_cap;
+    }
+    return DCOL_SUCCESS;
+}
+
 // Returns 0 when fused (or not allowed), 1 when the plan does not qualify (large or
 // single-variant), 2 when it qualifies but a bucket has no case in the fused kernel.
 int plan_fuse(const dcol_table* t, dcol_plan* p, bool allow) {
@@ -537,7 +592,7 @@ int dcol_plan_create(const dcol_table* t, int64_t B, const int32_t* s1, const in
 int dcol_plan_create_ex(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, int32_t options,
                         dcol_plan** out) {
     if (!t || !out || B < 0 || (B > 0 && (!s1 || !s2))) return fail(DCOL_ERR_ARG, "dcol_plan_create: bad arguments");
-    if (options & ~(DCOL_PLAN_CASE4 | DCOL_PLAN_NO_FUSE))
+    if (options & ~(DCOL_PLAN_CASE4 | DCOL_PLAN_NO_FUSE | DCOL_PLAN_SUSPEND))
         return fail(DCOL_ERR_ARG, "dcol_plan_create_ex: unknown option bits");
     if (B > INT32_MAX) return fail(DCOL_ERR_ARG, "dcol_plan_create: B exceeds 2^31-1");
     *out = nullptr;
@@ -573,6 +628,7 @@ int dcol_plan_create_ex(const dcol_table* t, int64_t B, const int32_t* s1, const
         return fail(DCOL_ERR_HIP, std::string("dcol_plan_create: ") + hipGetErrorString(e));
     }
     rc = ensure_fanout(t, p);
+    if (rc == DCOL_SUCCESS && (options & DCOL_PLAN_SUSPEND)) rc = plan_susp(t, p);
     if (rc != DCOL_SUCCESS) {
         dcol_plan_destroy(p);
         return rc;
@@ -589,8 +645,24 @@ int dcol_plan_destroy(dcol_plan* p) {
         if (p->d_s2) (void)hipFree(p->d_s2);
         if (p->d_perm) (void)hipFree(p->d_perm);
         if (p->d_segs) (void)hipFree(p->d_segs);
+        if (p->d_susp) (void)hipFree(p->d_susp);
     }
     delete p;
+    return DCOL_SUCCESS;
+}
+
+int dcol_plan_suspended(const dcol_plan* p, int64_t* n) {
+    if (!p || !n) return fail(DCOL_ERR_ARG, "dcol_plan_suspended: NULL argument");
+    *n = 0;
+    if (!p->d_susp) return DCOL_SUCCESS;
+    DeviceGuard g(p->table->device);
+    for (const Launch& L : p->launches) {
+        if (!L.susp) continue;
+        int32_t c = 0;
+        const hipError_t e = hipMemcpy(&c, L.d_susp_count, sizeof(c), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_plan_suspended: ") + hipGetErrorString(e));
+        *n += c;
+    }
     return DCOL_SUCCESS;
 }
 
@@ -637,6 +709,12 @@ int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, 
     a.grad = grad;
     a.iters = iters;
     a.status = status;
+    a.susp_t = 0;
+    a.susp_min = 0;
+    a.susp_count = nullptr;
+    a.susp_pi = nullptr;
+    a.susp_state = nullptr;
+    a.susp_cap = 0;
     const bool fan = p->lanes > 1 && p->fork;
     hipError_t e = hipSuccess;
     if (fan) {
@@ -653,6 +731,16 @@ int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, 
             const int64_t grid = (L.n + kBlock - 1) / kBlock;
             hipLaunchKernelGGL(reject_kernel, dim3(grid), dim3(kBlock), 0, ls, a, L.code);
             e = hipGetLastError();
+        } else if (L.susp) {   // main + resume launch pair (plan_susp)
+            KArgs b = a;
+            b.susp_t = susp_t_env();
+            b.susp_min = susp_min_env();
+            b.susp_count = L.d_susp_count;
+            b.susp_pi = L.d_susp_pi;
+            b.susp_state = L.d_susp_state;
+            b.susp_cap = L.susp_cap;
+            e = hipMemsetAsync(L.d_susp_count, 0, sizeof(int32_t), ls);
+            if (e == hipSuccess) e = launch_susp(L.N, L.nsoc, L.omax, L.lpp, L.flags(), L.oe, b, ls);
         } else {
             e = launch_variant(L.N, L.nsoc, L.omax, L.lpp, L.flags(), a, ls, L.oe);
         }
@@ -738,8 +826,35 @@ int dcol_debug_exec_violations(uint64_t* out, int32_t reset) {
     uint64_t total = 0;
 #define DCOL_EXEC_SUM(tag) total += exec_violations_##tag(reset != 0);
     DCOL_EXEC_TAGS(DCOL_EXEC_SUM)
+    DCOL_EXEC_SUM(capi)
 #undef DCOL_EXEC_SUM
     *out = total;
+    return DCOL_SUCCESS;
+}
+#endif
+
+#ifdef DCOL_CHECK_EXEC
+}  // extern "C"
+namespace dcol {
+// positive control of the DPP-source check: in each wave the odd lanes leave, then the even
+// lanes take a 2-lane group sum whose partner lane is inactive -- 32 counted reads per wave
+__global__ void __launch_bounds__(64) exec_selftest_kernel(double* out) {
+    const int l = (int)threadIdx.x;
+    if (l & 1) return;
+    out[l] = Grp<2>::sum((double)l);
+}
+DCOL_EXEC_READER(capi)
+}  // namespace dcol
+extern "C" {
+int dcol_debug_exec_selftest(uint64_t* counted) {
+    if (!counted) return fail(DCOL_ERR_ARG, "dcol_debug_exec_selftest: NULL out");
+    double* d = nullptr;
+    if (hipMalloc(&d, 64 * sizeof(double)) != hipSuccess) return fail(DCOL_ERR_HIP, "selftest alloc");
+    (void)exec_violations_capi(true);
+    hipLaunchKernelGGL(exec_selftest_kernel, dim3(1), dim3(64), 0, 0, d);
+    (void)hipDeviceSynchronize();
+    *counted = exec_violations_capi(true);
+    (void)hipFree(d);
     return DCOL_SUCCESS;
 }
 #endif

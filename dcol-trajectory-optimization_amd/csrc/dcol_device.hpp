@@ -95,6 +95,7 @@ DCOL_HD bool pos_finite(double x) {
 }
 
 enum : int32_t { ST_OK = 0, ST_MAXITER = 1, ST_UNSUPPORTED = 2, ST_NOT_PD = 3, ST_NONFINITE = 4, ST_TOO_LARGE = 5 };
+constexpr int32_t ST_SUSPENDED = 100;   // internal: handed to the resume launch (never reported)
 enum : int32_t { SOC_NONE = 0, SOC_BALL = 1, SOC_CONE = 2 };
 enum : int32_t { F_GRAD_FD = 1, F_GRAD_ENV = 2, F_CONTACT = 4, F_GRAD_IMP = 16 };
 
@@ -150,6 +151,17 @@ struct KArgs {
     double* __restrict__ grad;          // [12][B]
     int32_t* __restrict__ iters;        // [B]
     int32_t* __restrict__ status;       // [B]
+    // Suspend / resume (variants with FL bit 4; dcol_capi.cpp): in the main launch, a wave
+    // whose still-iterating pairs drop to susp_t or fewer, at iteration susp_min or later,
+    // hands those pairs -- their iterate (x, s, z, r) and iteration count -- to the resume
+    // launch, which reassembles their rows and continues the same iteration sequence.  One
+    // entry per suspended pair; at most susp_t per wave, so susp_cap = waves * susp_t suffices.
+    int32_t susp_t;                     // 0: never suspend
+    int32_t susp_min;
+    int32_t* susp_count;                // entries appended (zeroed before the main launch)
+    int32_t* susp_pi;                   // [susp_cap] pair index (slot index into perm space)
+    double* susp_state;                 // [fields][susp_cap]: it, x[N], then (s, z, r) per lane row
+    int64_t susp_cap;
 #ifdef DCOL_STAMPS
     unsigned long long* stamps;         // diagnostic build only (tools/stamp_probe.hip): [B][16]
 #endif
@@ -431,7 +443,6 @@ DCOL_HD double soc_ls_inv(const double* y, const double* d, double isn, double r
 // Butterflies with commutative adds: every lane of a group ends with the bitwise same
 // value, so the replicated scalar part of the method (Cholesky, mu, sigma, step) takes
 // identical decisions in every lane of the pair.
-#if defined(__HIP_DEVICE_COMPILE__)
 #ifdef DCOL_CHECK_EXEC
 // Diagnostic build (make check-exec, lib_check/): every DPP read whose source lane is
 // inactive is counted -- the only way a reduction could read a register the program never
@@ -440,6 +451,9 @@ DCOL_HD double soc_ls_inv(const double* y, const double* d, double isn, double r
 // one counter per translation unit (no relocatable device code): dcol_launch.hpp
 // DCOL_EXEC_READER reads it back
 static __device__ unsigned long long dcol_exec_violations;
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+#ifdef DCOL_CHECK_EXEC
 template <int CTRL>
 __device__ __forceinline__ void dpp_check() {
     const unsigned lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -1126,8 +1140,10 @@ struct Solver {
     template <bool FULL>
     DCOL_HD bool live(int k) const { return FULL || vort(k); }
 
-    template <bool FULL>
-    DCOL_HD int32_t pdip(double tol, int max_iter, int* it_out) {
+    // it0: first iteration (a resumed pair continues its count); susp_t > 0: suspension
+    // check (SUSP main launch) -- see KArgs
+    template <bool FULL, bool SUSP = false>
+    DCOL_HD int32_t pdip(double tol, int max_iter, int* it_out, int it0 = 0, int susp_t = 0, int susp_min = 0) {
         int it = 0;
         int32_t st = ST_MAXITER;
         // mu = s'z / deg as a multiply by the correctly rounded 1/deg plus one FMA remainder
@@ -1135,7 +1151,7 @@ struct Solver {
         // per iteration
         const double degd = FULL ? (double)(OMAX + NSOC) : (double)deg;
         const double rdeg = 1.0 / degd;
-        for (it = 0; it < max_iter; ++it) {
+        for (it = it0; it < max_iter; ++it) {
             DCOL_ISTAMP(it, 0);
             // ---- mu = s'z / deg and the exit test first (pdip.py:410-422, quirk Q3): the
             // iteration that returns does not build the normal matrix
@@ -1164,6 +1180,17 @@ struct Solver {
                 st = ST_OK;
                 break;
             }
+#if defined(__HIP_DEVICE_COMPILE__)
+            if constexpr (SUSP) {
+                // the lanes still in the loop (every lane of a live pair; the decision is
+                // wave-uniform, so a pair's lanes suspend together)
+                if (it >= susp_min && susp_t > 0 &&
+                    __builtin_popcountll(__builtin_amdgcn_ballot_w64(true)) <= susp_t * LPP) {
+                    st = ST_SUSPENDED;
+                    break;
+                }
+            }
+#endif
             // ---- NT scalings, residuals, normal matrix (pdip.py:410-434)
             SocState so[SSA];
             double Hm[N][N];
@@ -1429,6 +1456,65 @@ struct Solver {
         const int k0 = OR + SD * b;
         const double ib = fmax(soc_ls_inv<SD>(s + k0, ds, W.lis[0], W.lrc[0]), soc_ls_inv<SD>(z + k0, dz, W.lis[1], W.lrc[1]));
         return vs[b] ? fmax(cmax, ib) : cmax;
+    }
+
+    // -------- suspend / resume (KArgs susp_*) --------------------------------------------
+    // fields of a suspended pair's entry: it, x[N], then (s, z, r) of every lane row
+    static constexpr int SUSP_FIELDS = 1 + N + 3 * M * LPP;
+    DCOL_HD static int64_t sfield(int k, int q, int c) { return 1 + N + ((int64_t)(k * LPP + q) * 3 + c); }
+    // Main launch, after pdip: the pairs that returned ST_SUSPENDED take consecutive entries
+    // (one atomic per wave); true for their lanes, which then return.  Every lane of the wave
+    // runs this (wave-level ballot).
+    DCOL_HD bool suspend(const KArgs& A, int64_t pi, int32_t st, int it) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const bool me = st == ST_SUSPENDED;
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(me);
+        if (m == 0ull) return false;
+        constexpr unsigned long long lead_pat = LPP == 1 ? ~0ull : LPP == 2 ? 0x5555555555555555ull
+                                              : LPP == 4 ? 0x1111111111111111ull : LPP == 8 ? 0x0101010101010101ull
+                                                                                 : 0x0001000100010001ull;
+        const unsigned long long lead = m & lead_pat;
+        const unsigned lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        const int first = __builtin_ctzll(m);
+        int base = 0;
+        if ((int)lane == first) base = atomicAdd(A.susp_count, __builtin_popcountll(lead));
+        base = __builtin_amdgcn_readlane(base, first);
+        if (!me) return false;
+        const unsigned l0 = lane - (unsigned)q;   // the pair's first lane
+        const int64_t ci = base + __builtin_popcountll(lead & ((1ull << l0) - 1ull));
+        const int64_t cap = A.susp_cap;
+        double* __restrict__ o = A.susp_state;
+        if (q == 0) {
+            A.susp_pi[ci] = (int32_t)pi;
+            o[ci] = (double)it;
+#pragma unroll
+            for (int j = 0; j < N; ++j) o[(1 + j) * cap + ci] = x[j];
+        }
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+            o[sfield(k, q, 0) * cap + ci] = s[k];
+            o[sfield(k, q, 1) * cap + ci] = z[k];
+            o[sfield(k, q, 2) * cap + ci] = r[k];
+        }
+        return true;
+#else
+        (void)A; (void)pi; (void)st; (void)it;
+        return false;
+#endif
+    }
+    // Resume launch: the entry's iterate in place of initialize(); returns its iteration count
+    DCOL_HD int load_state(const KArgs& A, int64_t ci) {
+        const int64_t cap = A.susp_cap;
+        const double* __restrict__ o = A.susp_state;
+#pragma unroll
+        for (int j = 0; j < N; ++j) x[j] = o[(1 + j) * cap + ci];
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+            s[k] = o[sfield(k, q, 0) * cap + ci];
+            z[k] = o[sfield(k, q, 1) * cap + ci];
+            r[k] = o[sfield(k, q, 2) * cap + ci];
+        }
+        return (int)o[ci];
     }
 
     // -------- gradient helpers ---------------------------------------------------------
@@ -1730,8 +1816,11 @@ DCOL_HD void launder(P& p) {
 // FULL: every pair of the launch has o == OMAX (no padding rows); BALL: every SOC block of
 // the launch is a ball block (Solver).  The host picks the variant per launch
 // (dcol_capi.cpp: bucket_pairs).
-template <int N, int NSOC, int OMAX, int LPP, bool FULL = false, bool BALL = false, bool CONE = false, int OE = 0>
-DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
+// MODE 0: one launch; 1: main launch of a suspend / resume pair (KArgs susp_*); 2: the
+// resume launch, for continuation entry ci (pi = its pair)
+template <int N, int NSOC, int OMAX, int LPP, bool FULL = false, bool BALL = false, bool CONE = false, int OE = 0,
+          int MODE = 0>
+DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1) {
     DCOL_STAMP(A, pi, q, 0);
     const int64_t B = A.B;
     const int k1 = A.s1[pi], k2 = A.s2[pi];
@@ -1757,11 +1846,19 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q) {
     DCOL_STAMP(A, pi, q, 2);
     int it = 0;
     int32_t st;
-    const bool init_ok = P.initialize();
-    DCOL_STAMP(A, pi, q, 3);
-    if (!init_ok) st = ST_NOT_PD;
-    else st = P.template pdip<FULL>(A.tol, A.max_iter, &it);
+    if constexpr (MODE == 2) {   // continue the suspended iteration sequence
+        const int it0 = P.load_state(A, ci);
+        st = P.template pdip<FULL>(A.tol, A.max_iter, &it, it0);
+    } else {
+        const bool init_ok = P.initialize();
+        DCOL_STAMP(A, pi, q, 3);
+        if (!init_ok) st = ST_NOT_PD;
+        else st = P.template pdip<FULL, MODE == 1>(A.tol, A.max_iter, &it, 0, A.susp_t, A.susp_min);
+    }
     DCOL_STAMP(A, pi, q, 4);
+    if constexpr (MODE == 1) {
+        if (P.suspend(A, pi, st, it)) return;   // the resume launch finishes this pair
+    }
 
     const double nan = __builtin_nan("");
     const bool ok = st == ST_OK;
@@ -1872,7 +1969,8 @@ constexpr int kSolveBlock = DCOL_BLOCK;
 static_assert(kSolveBlock % 64 == 0, "one or more whole waves per workgroup");
 
 // FL: variant flags, bit 0 FULL, bit 1 BALL, bit 2 CONE (variants.py)
-// OE > 0: the row-partitioned (PART) copy with OE extra-column row slots (Solver)
+// OE > 0: the row-partitioned (PART) copy with OE extra-column row slots (Solver).
+// FL bit 4 (16): the main launch of a suspend / resume pair (solve_one MODE 1)
 template <int N, int NSOC, int OMAX, int LPP, int WPS, int FL, int OE = 0>
 __global__ void __launch_bounds__(kSolveBlock, WPS) prox_kernel(KArgs A) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1880,7 +1978,19 @@ __global__ void __launch_bounds__(kSolveBlock, WPS) prox_kernel(KArgs A) {
     const int q = (int)(t % LPP);
     if (slot >= A.n) return;
     const int64_t pi = A.perm ? (int64_t)A.perm[A.slot0 + slot] : (A.slot0 + slot);
-    solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0, OE>(A, pi, q);
+    solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0, OE, (FL & 16) ? 1 : 0>(A, pi, q);
+}
+
+// The resume launch of a suspend / resume pair: one lane group per continuation entry;
+// entries past the count the main launch appended exit at once.
+template <int N, int NSOC, int OMAX, int LPP, int WPS, int FL, int OE = 0>
+__global__ void __launch_bounds__(kSolveBlock, WPS) prox_resume_kernel(KArgs A) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t ci = t / LPP;
+    const int q = (int)(t % LPP);
+    if (ci >= A.susp_cap || ci >= (int64_t)*A.susp_count) return;
+    const int64_t pi = A.susp_pi[ci];
+    solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0, OE, 2>(A, pi, q, ci);
 }
 
 }  // namespace dcol

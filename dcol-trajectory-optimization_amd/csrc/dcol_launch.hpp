@@ -27,6 +27,9 @@ struct FusedSeg {
     int64_t block0, slot0, n;
 };
 constexpr int kMaxFusedSegs = 64;
+// suspend / resume launch pairs (dcol_kernels_susp.hip)
+bool susp_available(int N, int nsoc, int omax, int lpp, int flags, int oe, int* fields);
+hipError_t launch_susp(int N, int nsoc, int omax, int lpp, int flags, int oe, const KArgs& args, hipStream_t stream);
 // fused variant id of a kernel shape + (lpp, launch flags, PART extra slots oe), or -1 if
 // the fused kernel lacks it
 int fused_vid(int N, int nsoc, int omax, int lpp, int flags, int oe = 0);
@@ -42,9 +45,10 @@ hipError_t launch_fused(const KArgs& args, const FusedSeg* d_segs, int nseg, int
         if (reset) (void)hipMemcpyToSymbol(HIP_SYMBOL(dcol_exec_violations), &z, sizeof(z));   \
         return v;                                                                              \
     }
-#define DCOL_EXEC_TAGS(X) X(n4) X(n5) X(n6) X(n7) X(n8) X(fused) X(p51) X(p52) X(p61) X(p62)
+#define DCOL_EXEC_TAGS(X) X(n4) X(n5) X(n6) X(n7) X(n8) X(fused) X(p51) X(p52) X(p61) X(p62) X(susp)
 #define DCOL_EXEC_DECL(tag) unsigned long long exec_violations_##tag(bool reset);
 DCOL_EXEC_TAGS(DCOL_EXEC_DECL)
+DCOL_EXEC_DECL(capi)   // the C-ABI unit's own counter (dcol_debug_exec_selftest)
 #undef DCOL_EXEC_DECL
 #else
 #define DCOL_EXEC_READER(tag)

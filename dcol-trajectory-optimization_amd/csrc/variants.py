@@ -46,6 +46,13 @@ Generates dcol_variants.inc (FL = variant flags: bit 0 FULL, bit 1 BALL, bit 2 C
   DCOL_PART_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, FL, OE) the row-partitioned copies
   DCOL_PART_SHAPES(X)    X(N, NSOC, OMAX, OE) once per PART bucket (host bucketing, emulator)
   DCOL_FUSED_PART_VARIANTS(X)  X(ID, N, NSOC, OMAX, LPP, FL, OE) the PART cases of the fused kernel
+  DCOL_SUSP_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, FL, OE) suspend / resume copies (FL bit 4 = 16)
+
+SUSP variants (dcol_device.hpp KArgs susp_*, dcol_kernels_susp.hip): a large launch runs as a
+main launch in which a wave hands its last few iterating pairs (<= DCOL_SUSPEND_T of 32, after
+DCOL_SUSPEND_MIN iterations) to a compact resume launch, instead of running every lane of
+the wave until its slowest pair converges.  Results are bitwise those of the one-launch
+kernel (the same iteration sequence, continued from the saved iterate).
 
 PART variants (row partition, dcol_device.hpp Solver<..., OE>): N = 5 / 6 pairs of combine
 cases 1-3 (one primitive with extra columns) whose pose rows (polytope faces, cone base,
@@ -60,7 +67,7 @@ import os
 
 OMAX = {
     (4, 0): [4, 8, 12, 16, 24, 32, 48, 64, 128],     # polytope x polytope
-    (4, 1): [2, 4, 6, 8, 12, 16, 24, 32, 48, 64, 128],  # polytope x {sphere, cone}
+    (4, 1): [2, 4, 6, 7, 8, 12, 16, 24, 32, 48, 64, 128],  # polytope x {sphere, cone}; 7: cone x box
     (4, 2): [2],                        # {sphere, cone} x {sphere, cone}
     (5, 1): [8, 10, 12, 16, 24, 32, 48, 64, 128],    # {capsule, cylinder} x polytope
     (5, 2): [2, 4, 6, 8],               # {capsule, cylinder} x {sphere, cone}
@@ -81,6 +88,7 @@ CONFIG = {
     (4, 1, 2): [(2, 1)],
     (4, 1, 4): [(1, 1), (2, 2), (4, 2)],
     (4, 1, 6): [(2, 2), (1, 1)],        # sphere x box: 2 waves/SIMD spill-free with ball rows
+    (4, 1, 7): [(1, 1)],                # cone x box (1 + 6 rows): no padding slot at LPP 1
     (4, 1, 8): [(1, 1), (2, 1), (8, 2)],
     (4, 1, 12): [(2, 1), (4, 1)],
     (4, 2, 2): [(2, 2)],
@@ -101,6 +109,9 @@ CONFIG = {
 # footprint differs from the dense kernel's, so their spill-free (LPP, WPS) can too
 CONFIG_FL = {}
 FULL = {(4, 0)}   # shapes with padding-free copies (see module docstring)
+# padding-free copies of the structured-cone kernels: (N, NSOC, OMAX) whose pairs commonly
+# fill the bucket (cone x box: the cone's base row + 6 faces = 7)
+FULL_CONE = {(4, 1, 7)}
 
 
 def ball(n, nsoc):
@@ -170,6 +181,9 @@ def part_variants():
             for fl in part_flavours(n, s) for l, w in cf]
 
 
+# (N, NSOC, OMAX, LPP, WPS, FL without the SUSP bit, OE): the benchmark's poly x poly kernel
+SUSP = [(4, 0, 12, 2, 2, 1, 0)]
+
 FUSE_PART_OMAX = 6   # PART buckets in the fused kernel: the small ones (its compile time grows with its cases)
 
 
@@ -215,6 +229,9 @@ def main():
     lines += [f"    X({n}, {s}, {o}, {l}, {w}, 0) \\" for n, s, o in shapes for l, w in configs(n, s, o)]
     lines += ["", "#define DCOL_FULL_VARIANTS(X) \\"]
     lines += [f"    X({n}, {s}, {o}, {l}, {w}, 1) \\" for n, s, o in shapes if (n, s) in FULL for l, w in configs(n, s, o)]
+    lines += ["", "#define DCOL_FULL_CONE_VARIANTS(X) \\"]
+    lines += [f"    X({n}, {s}, {o}, {l}, {w}, 5) \\" for n, s, o in shapes if (n, s, o) in FULL_CONE
+              for l, w in configs_fl(n, s, o, 4)]
     lines += ["", "#define DCOL_BALL_VARIANTS(X) \\"]
     lines += [f"    X({n}, {s}, {o}, {l}, {w}, 2) \\" for n, s, o in shapes if ball(n, s)
               for l, w in configs_fl(n, s, o, 2) if (n, s, o, l) not in BALL_SKIP]
@@ -232,6 +249,8 @@ def main():
     lines += ["", "#define DCOL_FUSED_PART_VARIANTS(X) \\"]
     base = len(fused())
     lines += [f"    X({base + i}, {n}, {s}, {o}, {l}, {f}, {oe}) \\" for i, (n, s, o, l, f, oe) in enumerate(fused_part())]
+    lines += ["", "#define DCOL_SUSP_VARIANTS(X) \\"]
+    lines += [f"    X({n}, {s}, {o}, {l}, {w}, {fl | 16}, {oe}) \\" for n, s, o, l, w, fl, oe in SUSP]
     lines.append("")
     out = os.path.join(here, "dcol_variants.inc")
     txt = "\n".join(lines) + "\n"

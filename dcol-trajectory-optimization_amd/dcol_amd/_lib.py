@@ -20,7 +20,7 @@ OK, MAXITER, UNSUPPORTED, NOT_PD, NONFINITE, TOO_LARGE = range(6)
 GRAD_FD, GRAD_ENVELOPE, CONTACT, CASE4, GRAD_IMPLICIT = 1, 2, 4, 8, 16
 GRAD_ANY = GRAD_FD | GRAD_ENVELOPE | GRAD_IMPLICIT
 # enum dcol_plan_options
-PLAN_CASE4, PLAN_NO_FUSE = 1, 2
+PLAN_CASE4, PLAN_NO_FUSE, PLAN_SUSPEND = 1, 2, 4
 SUCCESS, ERR_ARG, ERR_HIP, ERR_NOMEM = 0, -1, -2, -3
 ABI_VERSION = 2
 
@@ -52,6 +52,7 @@ SIGNATURES = {
     "dcol_plan_destroy": (c_int, [c_void_p]),
     "dcol_plan_num_launches": (c_int, [c_void_p, POINTER(c_int32)]),
     "dcol_plan_num_buckets": (c_int, [c_void_p, POINTER(c_int32)]),
+    "dcol_plan_suspended": (c_int, [c_void_p, POINTER(c_int64)]),
     "dcol_plan_run": (c_int, [c_void_p, c_void_p, c_void_p, c_double, c_int32, c_int32, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_void_p]),
     "dcol_prox_batch_host": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_double,

@@ -105,10 +105,12 @@ class Table:
 class Plan:
     """Owning wrapper of a dcol_plan: a fixed pairing bucketed by kernel variant."""
 
-    def __init__(self, table: Table, s1, s2, case4: bool = False, fuse: bool = True):
+    def __init__(self, table: Table, s1, s2, case4: bool = False, fuse: bool = True, suspend: bool = False):
         """case4=True: solve case-4 pairs (DCOL_PLAN_CASE4 extension) instead of reporting
         UNSUPPORTED like the reference.  fuse=False: one launch per variant bucket even for
-        a small mixed plan (DCOL_PLAN_NO_FUSE; A/B and tests)."""
+        a small mixed plan (DCOL_PLAN_NO_FUSE; A/B and tests).  suspend=True: large buckets
+        run as a suspend / resume launch pair (DCOL_PLAN_SUSPEND; bitwise the same results;
+        the plan owns scratch -- do not run it on two streams at once)."""
         lib = _lib.load()
         self.s1 = np.ascontiguousarray(s1, dtype=np.int32)
         self.s2 = np.ascontiguousarray(s2, dtype=np.int32)
@@ -118,7 +120,8 @@ class Plan:
         self.B = int(self.s1.size)
         h = ctypes.c_void_p()
         self.case4 = bool(case4)
-        opts = (_lib.PLAN_CASE4 if case4 else 0) | (0 if fuse else _lib.PLAN_NO_FUSE)
+        opts = (_lib.PLAN_CASE4 if case4 else 0) | (0 if fuse else _lib.PLAN_NO_FUSE) | (
+            _lib.PLAN_SUSPEND if suspend else 0)
         _lib.check(lib.dcol_plan_create_ex(table.handle, self.B, _np_ptr(self.s1), _np_ptr(self.s2),
                                            opts, ctypes.byref(h)), "dcol_plan_create_ex")
         self.handle = h
@@ -127,6 +130,12 @@ class Plan:
         self.num_launches = int(n.value)       # kernel launches per run
         _lib.check(lib.dcol_plan_num_buckets(h, ctypes.byref(n)), "dcol_plan_num_buckets")
         self.num_buckets = int(n.value)        # variant buckets (incl. rejected pairs)
+
+    def suspended(self) -> int:
+        """pairs the last completed run handed to resume launches (synchronise first)"""
+        n = ctypes.c_int64()
+        _lib.check(_lib.load().dcol_plan_suspended(self.handle, ctypes.byref(n)), "dcol_plan_suspended")
+        return int(n.value)
 
     def run(self, pose1, pose2, tol=DEFAULT_TOL, max_iter=DEFAULT_MAX_ITER, grad="fd", contact=True,
             out=None, stream=None):
@@ -258,11 +267,11 @@ class Engine:
                 self._table = Table(self._specs, self.device)
             return self._table
 
-    def plan(self, s1, s2, cache=True, case4=False, fuse=True) -> Plan:
+    def plan(self, s1, s2, cache=True, case4=False, fuse=True, suspend=False) -> Plan:
         s1 = np.ascontiguousarray(s1, dtype=np.int32)
         s2 = np.ascontiguousarray(s2, dtype=np.int32)
-        if not cache:
-            return Plan(self.table, s1, s2, case4, fuse)
+        if not cache or suspend:   # suspend plans own scratch: never shared through the cache
+            return Plan(self.table, s1, s2, case4, fuse, suspend)
         key = (s1.tobytes(), s2.tobytes(), bool(case4), bool(fuse))
         with self._lock:
             p = self._plans.get(key)

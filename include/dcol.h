@@ -85,10 +85,16 @@ enum dcol_plan_options {
                            them — are assembled with primitive 2's extra columns placed after
                            primitive 1's (n = 4 + e1 + e2 <= 8) and solved by the same PDIP.
                            Without the option they get DCOL_UNSUPPORTED like the reference. */
-    DCOL_PLAN_NO_FUSE = 2 /* always one launch per bucket.  By default a plan with several
+    DCOL_PLAN_NO_FUSE = 2, /* always one launch per bucket.  By default a plan with several
                            buckets (kernel variants) whose pairs together fill less than one
                            wave per SIMD -- an ALTRO phase batch -- runs every bucket in ONE
                            fused launch (no stream fan-out); results are bitwise the same.  */
+    DCOL_PLAN_SUSPEND = 4 /* large buckets with a suspend / resume kernel pair run as a main
+                           launch in which each wave hands its last few iterating pairs to a
+                           compact resume launch, instead of idling most of its lanes until
+                           its slowest pair converges; results are bitwise the same.  The plan
+                           then owns device scratch written by every run: do not run it on
+                           two streams at once (one plan per stream).                       */
 };
 
 /* Return codes of every entry point. */
@@ -139,6 +145,9 @@ int dcol_plan_create_ex(const dcol_table* table, int64_t B, const int32_t* shape
 int dcol_plan_destroy(dcol_plan* plan);
 int dcol_plan_num_launches(const dcol_plan* plan, int32_t* n); /* kernel launches per run */
 int dcol_plan_num_buckets(const dcol_plan* plan, int32_t* n);  /* variant buckets (incl. rejects) */
+/* DCOL_PLAN_SUSPEND plans: pairs the last completed run handed to resume launches
+ * (synchronous copy; call after the run's stream has been synchronised), else 0.       */
+int dcol_plan_suspended(const dcol_plan* plan, int64_t* n);
 
 /* Solve every pair of the plan.  All arrays are DEVICE pointers on the table's device,
  * structure-of-arrays:

@@ -260,3 +260,23 @@ def test_max_size_192m_pairs_position_independent():
         assert torch.equal(big["iters"][sl], base["iters"]), k
         assert torch.equal(big["alpha"][sl], base["alpha"]), k
         assert torch.equal(big["grad"][:, sl], base["grad"]), k
+
+
+def test_suspend_resume_bitwise_equal(batch):
+    """DCOL_PLAN_SUSPEND (opt-in): the benchmark batch as a main launch that hands each
+    wave's last few iterating pairs to a resume launch -- the same iteration sequence
+    continued from the saved iterate, so every output equals the one-launch plan bitwise;
+    and some pairs were actually suspended."""
+    import torch
+    b = batch
+    dev = torch.device("cuda", 0)
+    d1 = torch.from_numpy(np.ascontiguousarray(b["p1"].T)).to(dev)
+    d2 = torch.from_numpy(np.ascontiguousarray(b["p2"].T)).to(dev)
+    plain = b["eng"].plan(b["ids"][b["s1"]], b["ids"][b["s2"]], cache=False)
+    susp = b["eng"].plan(b["ids"][b["s1"]], b["ids"][b["s2"]], cache=False, suspend=True)
+    a = plain.run(d1, d2, grad="fd", contact=True)
+    c = susp.run(d1, d2, grad="fd", contact=True)
+    torch.cuda.synchronize()
+    assert susp.suspended() > 0
+    for k in ("status", "iters", "alpha", "grad", "contact"):
+        assert torch.equal(a[k], c[k]), k
