@@ -942,6 +942,68 @@ struct Solver {
             }
         }
     }
+    // Hm += G_b' W^-2 G_b, the SOC block's share of the normal matrix G~'G~ (pdip.py:434).
+    // Dense / CONE rows: through G~_b = W^-1 G_b (soc_gtilde).  BALL rows [0 0 0 -R | 0],
+    // [-e_k | 0 | X_k]: straight from the entries of M = W^-2 = eta^-2 J Wbar^2 J
+    // (M00 = e2 (2 w0^2 - 1), M0k = -2 e2 w0 w1_k, Mkl = e2 (d_kl + 2 w1_k w1_l)), so
+    //   H[j][c] = M(j+1,c+1), H[j][3] = R M(0,j+1), H[3][3] = R^2 M00 (j, c < 3),
+    //   H[j][4+i] = -(M' X)(j,i), H[3][4+i] = -R (M0' X)(i), H[4+i][4+i2] = X_i' M' X_i2
+    // with M' = M(1:,1:) -- the same matrix by fewer products (rounding-level).  An inert slot
+    // (sv = R = X = 0) adds zeros.
+    DCOL_HD void soc_hadd(int b, const SocNT& W, double (&Hm)[N][N]) const {
+        if constexpr (BALL) {
+            const double e2 = W.ieta * W.ieta;
+            const double tw = 2.0 * W.w0;
+            const double m00 = e2 * fma(tw, W.w0, -1.0);
+            const double et = e2 * tw;
+            double m0[3], mm[3][3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                m0[k] = -(et * W.w1[k]);
+#pragma unroll
+                for (int l = k; l < 3; ++l) {
+                    mm[k][l] = e2 * fma(2.0 * W.w1[k], W.w1[l], k == l ? 1.0 : 0.0);
+                    mm[l][k] = mm[k][l];
+                }
+            }
+            const double v = sv[b], R = sR[b];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+#pragma unroll
+                for (int c = j; c < 3; ++c) Hm[j][c] = fma(v, mm[j][c], Hm[j][c]);
+                Hm[j][3] = fma(v * R, m0[j], Hm[j][3]);
+            }
+            Hm[3][3] = fma(R * R, m00, Hm[3][3]);
+            if constexpr (NX > 0) {
+                double mx[3][NXA], m0x[NXA];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) {
+                    m0x[i] = m0[0] * sX[b][0][i] + m0[1] * sX[b][1][i] + m0[2] * sX[b][2][i];
+#pragma unroll
+                    for (int k = 0; k < 3; ++k)
+                        mx[k][i] = mm[k][0] * sX[b][0][i] + mm[k][1] * sX[b][1][i] + mm[k][2] * sX[b][2][i];
+                }
+#pragma unroll
+                for (int i = 0; i < NX; ++i) {
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) Hm[j][4 + i] = fma(-v, mx[j][i], Hm[j][4 + i]);
+                    Hm[3][4 + i] = fma(-R, m0x[i], Hm[3][4 + i]);
+#pragma unroll
+                    for (int i2 = i; i2 < NX; ++i2)
+                        Hm[4 + i][4 + i2] += sX[b][0][i] * mx[0][i2] + sX[b][1][i] * mx[1][i2] + sX[b][2][i] * mx[2][i2];
+                }
+            }
+        } else {
+            double gt[SD][N];
+            soc_gtilde(b, W, gt);
+#pragma unroll
+            for (int e = 0; e < SD; ++e)
+#pragma unroll
+                for (int j = 0; j < N; ++j)
+#pragma unroll
+                    for (int c = j; c < N; ++c) Hm[j][c] += gt[e][j] * gt[e][c];
+        }
+    }
     // upper Cholesky H = F'F (scipy.linalg.cholesky); false if a pivot is <= 0, infinite or
     // NaN.  Any non-finite entry of H's upper triangle makes some pivot non-finite (a
     // diagonal entry directly, an off-diagonal one through F[j][c]^2), so a non-finite H
@@ -1221,16 +1283,7 @@ struct Solver {
             }
             // SOC part of the normal matrix
 #pragma unroll
-            for (int b = 0; b < SS; ++b) {
-                double gt[SD][N];
-                soc_gtilde(b, so[b].W, gt);
-#pragma unroll
-                for (int e = 0; e < SD; ++e)
-#pragma unroll
-                    for (int j = 0; j < N; ++j)
-#pragma unroll
-                        for (int c = j; c < N; ++c) Hm[j][c] += gt[e][j] * gt[e][c];
-            }
+            for (int b = 0; b < SS; ++b) soc_hadd(b, so[b].W, Hm);
             allsum_sym(Hm);
             DCOL_ISTAMP(it, 1);
             double F[N][N], idg[N];
@@ -1357,17 +1410,28 @@ struct Solver {
         for (int b = 0; b < SS; ++b) {
             const int k0 = OR + SD * b;
             // W^-1 b~z = W^-1 W^-1 (-rz - W lds) = -W^-2 (s + r) - W^-1 lds   (rz = s + G x - h)
-            soc_lds(so[b], cp ? cp + k0 : nullptr, smu, slds[b]);
-            double m[SD], sr[SD], q[SD];
-            soc_solve<SD>(so[b].W, slds[b], m);
+            double sr[SD], q[SD], bz[SD];
 #pragma unroll
             for (int e = 0; e < SD; ++e) sr[e] = s[k0 + e] + r[k0 + e];
             soc_w2inv<SD>(so[b].W, sr, q);
+            if (!cp) {
+                // predictor: lambda \ ds = -lambda, so W^-1 lds = -W^-1 W z = -z exactly:
+                // W^-1 b~z = z - W^-2 (s + r) and (W^-1 b~z) - z = -W^-2 (s + r) (no soc_solve)
 #pragma unroll
-            for (int e = 0; e < SD; ++e) sbzt[b][e] = -q[e] - m[e];
-            double bz[SD];
+                for (int e = 0; e < SD; ++e) {
+                    slds[b][e] = -so[b].lam[e];
+                    sbzt[b][e] = z[k0 + e] - q[e];
+                    bz[e] = -q[e];
+                }
+            } else {
+                soc_lds(so[b], cp + k0, smu, slds[b]);
+                double m[SD];
+                soc_solve<SD>(so[b].W, slds[b], m);
 #pragma unroll
-            for (int e = 0; e < SD; ++e) bz[e] = sbzt[b][e] - z[k0 + e];
+                for (int e = 0; e < SD; ++e) sbzt[b][e] = -q[e] - m[e];
+#pragma unroll
+                for (int e = 0; e < SD; ++e) bz[e] = sbzt[b][e] - z[k0 + e];
+            }
             soc_gtv(b, bz, rhs);
         }
         allsum_vec(rhs);
@@ -1727,14 +1791,7 @@ struct Solver {
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
             soc_nt<SD>(s + OR + SD * b, z + OR + SD * b, W[b]);
-            double gt[SD][N];
-            soc_gtilde(b, W[b], gt);
-#pragma unroll
-            for (int e = 0; e < SD; ++e)
-#pragma unroll
-                for (int j = 0; j < N; ++j)
-#pragma unroll
-                    for (int c = j; c < N; ++c) Hm[j][c] += gt[e][j] * gt[e][c];
+            soc_hadd(b, W[b], Hm);
         }
         allsum_sym(Hm);
         double F[N][N], idg[N], e3[N];
