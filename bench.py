@@ -195,7 +195,19 @@ def main():
                     help="timed steps of the configs[4] sub-measurement (mixed1m) of the default line; 0 = skip")
     ap.add_argument("--torch-gather", action="store_true",
                     help="mixed1m: all-gather through torch.distributed instead of the C-ABI RCCL path")
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="GPU_MAX_HW_QUEUES for this process (HIP hardware queues; 0 = leave the environment's)")
+    ap.add_argument("--pack-pass", action="store_true",
+                    help="mixed1m: per-pair arrays + pack_records kernel + out-of-place all-gather instead of "
+                         "records written by the solver kernels with the all-gather in place (A/B)")
     args = ap.parse_args()
+    if args.hw_queues > 0:
+        # HIP runtime tunable, read at its initialisation (before any GPU call of this process
+        # and inherited by spawned ranks): the pipelined steps run on two caller streams plus
+        # the library's three side streams; with the default 4 hardware queues two of those
+        # share a queue, and a join barrier of one step then stalls the next step's kernels
+        # behind it
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # N ranks requested without a launcher: start them, before this process touches the GPU
@@ -332,6 +344,7 @@ def main():
                           if os.path.exists(os.path.join(REPO, "profiles", "flop_model.json")) else "hand model"},
         "pipeline": {"streams": S, "note": "steps issued round-robin on S streams with separate outputs; "
                      "value/ms_per_step are the pipelined throughput, serial_* the one-stream run",
+                     "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                      "serial_value": (B * world * args.steps / elapsed_serial) if elapsed_serial else value,
                      "serial_ms_per_step": 1e3 * (elapsed_serial or elapsed) / args.steps},
         "kernel_ms": kern_ms,
@@ -550,7 +563,9 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
                 comm.close()
                 comm, native_error = None, native_error or "another rank could not create its communicator"
         if comm is not None:
-            path = "C-ABI dcol_prox_batch_multi_gpu (pack_records + ncclAllGather, RCCL)"
+            path = ("C-ABI dcol_prox_batch_multi_gpu (pack_records + ncclAllGather, RCCL)" if args.pack_pass else
+                    "C-ABI dcol_prox_batch_multi_gpu in place (records written by the solver kernels into the "
+                    "gathered buffer, ncclAllGather in place, RCCL)")
     rec = torch.full((cap, REC), float("nan"), dtype=torch.float64, device=dev)
     gathered = torch.empty((world * cap, REC), dtype=torch.float64, device=dev if comm is not None else coll_dev)
 
@@ -583,8 +598,12 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
             o = out if j == 0 else alloc_outputs(n, dev, want_grad=True, want_contact=False)
             r_ = rec if j == 0 else torch.full((cap, REC), float("nan"), dtype=torch.float64, device=dev)
             g_ = gathered if j == 0 else torch.empty((world * cap, REC), dtype=torch.float64, device=dev)
-            lanes.append(lambda c=c, st=st, o=o, r_=r_, g_=g_: c.solve_gather(
-                plan, d1, d2, cap, grad=args.grad, out=o, stream=st, rec_local=r_, rec_all=g_))
+            if args.pack_pass:   # the pack kernel + out-of-place all-gather (A/B)
+                lanes.append(lambda c=c, st=st, o=o, r_=r_, g_=g_: c.solve_gather(
+                    plan, d1, d2, cap, grad=args.grad, out=o, stream=st, rec_local=r_, rec_all=g_))
+            else:                # records written by the solver kernels, all-gather in place
+                lanes.append(lambda c=c, st=st, g_=g_: c.solve_gather(
+                    plan, d1, d2, cap, grad=args.grad, stream=st, rec_all=g_, in_place=True, soa=False))
 
         def step():
             lanes[0]()
@@ -679,13 +698,16 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
         "solve_ms_rank0": solve_ms, "solve_ms_max_rank": solve_ms_max,
         "step_breakdown": {
             "note": "HIP events on each rank's launch stream, one step at a time (median of 10): solve = the "
-                    "plan run alone; step = solve + pack_records + all-gather; comm = step - solve",
+                    "plan run alone (per-pair arrays); step = the timed step (" + (
+                        "solve + pack_records + all-gather" if args.pack_pass else
+                        "solve writing the records into the gathered buffer + in-place all-gather") +
+                    "); comm = step - solve",
             "solve_ms_max_rank": solve_ms_max, "step_ms_max_rank": float(ranks_stats[:, 1].max()),
             "comm_ms_rank0": step_ms - solve_ms, "comm_frac_rank0": (step_ms - solve_ms) / step_ms if step_ms > 0 else None,
             "record_bytes_per_pair": REC * 8,
             "per_rank": {"solve_ms": ranks_stats[:, 0].tolist(), "step_ms": ranks_stats[:, 1].tolist(),
                          "iters_mean": ranks_stats[:, 2].tolist(), "pairs": ranks_stats[:, 3].astype(int).tolist()}},
-        "pipeline": {"streams": max(1, len(lanes)),
+        "pipeline": {"streams": max(1, len(lanes)), "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                      "serial_value": B * steps / elapsed_serial if elapsed_serial else B * steps / elapsed,
                      "serial_ms_per_step": 1e3 * (elapsed_serial or elapsed) / steps},
     }

@@ -81,6 +81,8 @@ bool device_side_streams(int dev, hipStream_t out[kSideStreams]) {
 
 }  // namespace
 
+static_assert(dcol::kRec == DCOL_REC, "record width");
+
 namespace dcol {
 // pairs rejected on the host (unsupported combination / too many rows)
 __global__ void __launch_bounds__(256) reject_kernel(KArgs A, int32_t code) {
@@ -89,13 +91,18 @@ __global__ void __launch_bounds__(256) reject_kernel(KArgs A, int32_t code) {
     const int64_t pi = A.perm ? (int64_t)A.perm[A.slot0 + t] : (A.slot0 + t);
     const int64_t B = A.B;
     const double nan = __builtin_nan("");
-    A.alpha[pi] = nan;
+    if (A.alpha) A.alpha[pi] = nan;
     if (A.iters) A.iters[pi] = 0;
     if (A.status) A.status[pi] = code;
     if ((A.flags & F_CONTACT) && A.contact)
         for (int q = 0; q < 3; ++q) A.contact[q * B + pi] = nan;
     if ((A.flags & (F_GRAD_FD | F_GRAD_ENV | F_GRAD_IMP)) && A.grad)
         for (int q = 0; q < 12; ++q) A.grad[q * B + pi] = nan;
+    if (A.rec) {
+        double* r = A.rec + (int64_t)kRec * pi;
+        for (int q = 0; q < 13; ++q) r[q] = nan;
+        r[13] = rec_ints(code, 0);
+    }
 }
 
 }  // namespace dcol
@@ -154,6 +161,7 @@ struct dcol_plan {
     bool owns = false;           // device arrays owned (false: views into table staging)
     std::vector<Launch> launches;
     int lanes = 1;               // streams the launches are spread over (1 = serial)
+    std::vector<int> issue;      // launch issue order (assign_lanes: longest first); empty = as built
     hipEvent_t fork = nullptr;   // recorded on the caller's stream, awaited by the side streams
     hipEvent_t join[kSideStreams] = {};
     // fused launch (small mixed plans): one segment per solve bucket, in launch order
@@ -444,29 +452,46 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
 // the chip; run back to back their latencies add up.  Spread them over the caller's stream
 // plus up to kSideStreams side streams (fork/join through events) — longest-first greedy on
 // a cost estimate (waves x per-pair work), reject launches stay on the caller's stream.
+// Per-pair cost of a solve bucket in ns at full occupancy (least-squares fit to the class
+// benchmark of profiles/r03_soc/class_bench.log, within ~17 % on the 13 SOC classes): row
+// slots, SOC blocks (dense SOC rows cost more than the structured ball / cone rows) and the
+// N x N normal-matrix work; polytope x polytope buckets run at two waves per SIMD (x 0.5).
+double bucket_cost(const Launch& L) {
+    const bool dense_soc = L.nsoc > 0 && !(L.flags() & (LF_BALL | LF_CONE));
+    const double per_pair = 0.0806 * L.omax + 0.127 * L.nsoc + 0.0139 * L.N * L.N + (dense_soc ? 0.143 * L.nsoc : 0.0);
+    return (double)L.n * per_pair * (L.nsoc == 0 ? 0.5 : 1.0);
+}
+
 void assign_lanes(dcol_plan* p) {
     int solves = 0;
     for (const Launch& L : p->launches) solves += L.kind == 0;
     p->lanes = 1;
+    p->issue.clear();
     if (solves < 2) return;
     const int lanes = std::min(solves, kSideStreams + 1);
     std::vector<int> order;
     std::vector<double> cost(p->launches.size(), 0.0);
     for (size_t i = 0; i < p->launches.size(); ++i) {
         const Launch& L = p->launches[i];
-        if (L.kind != 0) continue;
-        const double waves = std::ceil((double)L.n * L.lpp / 64.0);
-        cost[i] = waves * (double)(L.omax + 4 * L.nsoc + 2 * L.N) * (8.0 / L.lpp);
+        if (L.kind != 0) {
+            p->issue.push_back((int)i);   // rejects first, on the caller's stream
+            continue;
+        }
+        cost[i] = bucket_cost(L);
         order.push_back((int)i);
     }
-    std::sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+    // issued longest first: every stream starts on its biggest bucket and the short ones fill
+    // the tail, where the other streams' last kernels no longer occupy the whole chip
+    p->issue.insert(p->issue.end(), order.begin(), order.end());
     std::vector<double> load(lanes, 0.0);
     for (int i : order) {
         const int l = (int)(std::min_element(load.begin(), load.end()) - load.begin());
         p->launches[i].lane = l;
         load[l] += cost[i];
     }
-    p->lanes = lanes;
+    static const bool serial = std::getenv("DCOL_NO_FANOUT") != nullptr;   // A/B: one stream
+    p->lanes = serial ? 1 : lanes;
 }
 
 // A plan with several solve buckets that together leave the GPU mostly idle (fewer lanes
@@ -680,14 +705,20 @@ int dcol_plan_num_buckets(const dcol_plan* p, int32_t* n) {
     return DCOL_SUCCESS;
 }
 
-int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, double tol, int32_t max_iter,
-                  int32_t flags, double* alpha, double* contact, double* grad, int32_t* iters, int32_t* status,
-                  void* stream) {
+}  // extern "C"
+
+namespace {
+// dcol_plan_run with an optional record output (rec: [B][DCOL_REC], written by the solver
+// epilogues; then alpha / grad / iters / status may be NULL)
+int plan_run_rec(const dcol_plan* p, const double* pose1, const double* pose2, double tol, int32_t max_iter,
+                 int32_t flags, double* alpha, double* contact, double* grad, int32_t* iters, int32_t* status,
+                 double* rec, void* stream) {
     if (!p) return fail(DCOL_ERR_ARG, "dcol_plan_run: NULL plan");
     if (p->B == 0) return DCOL_SUCCESS;
-    if (!pose1 || !pose2 || !alpha) return fail(DCOL_ERR_ARG, "dcol_plan_run: pose1, pose2 and alpha are required");
+    if (!pose1 || !pose2 || (!alpha && !rec))
+        return fail(DCOL_ERR_ARG, "dcol_plan_run: pose1, pose2 and alpha are required");
     if ((flags & DCOL_CONTACT) && !contact) return fail(DCOL_ERR_ARG, "dcol_plan_run: DCOL_CONTACT needs contact[]");
-    if ((flags & DCOL_GRAD_ANY) && !grad) return fail(DCOL_ERR_ARG, "dcol_plan_run: gradient flag needs grad[]");
+    if ((flags & DCOL_GRAD_ANY) && !grad && !rec) return fail(DCOL_ERR_ARG, "dcol_plan_run: gradient flag needs grad[]");
     if (max_iter < 0) return fail(DCOL_ERR_ARG, "dcol_plan_run: max_iter < 0");
     const dcol_table* t = p->table;
     DeviceGuard g(t->device);
@@ -709,6 +740,7 @@ int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, 
     a.grad = grad;
     a.iters = iters;
     a.status = status;
+    a.rec = rec;
     a.susp_t = 0;
     a.susp_min = 0;
     a.susp_count = nullptr;
@@ -722,7 +754,9 @@ int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, 
         for (int l = 1; e == hipSuccess && l < p->lanes; ++l) e = hipStreamWaitEvent(t->side[l - 1], p->fork, 0);
         if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_plan_run fork: ") + hipGetErrorString(e));
     }
-    for (const Launch& L : p->launches) {
+    const size_t nl = p->launches.size();
+    for (size_t li = 0; li < nl; ++li) {
+        const Launch& L = p->launches[p->issue.size() == nl ? (size_t)p->issue[li] : li];
         if (L.kind == 0 && p->fused()) continue;   // covered by the fused launch below
         a.slot0 = L.slot0;
         a.n = L.n;
@@ -760,6 +794,15 @@ int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, 
     }
     if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_plan_run launch: ") + hipGetErrorString(e));
     return DCOL_SUCCESS;
+}
+}  // namespace
+
+extern "C" {
+
+int dcol_plan_run(const dcol_plan* p, const double* pose1, const double* pose2, double tol, int32_t max_iter,
+                  int32_t flags, double* alpha, double* contact, double* grad, int32_t* iters, int32_t* status,
+                  void* stream) {
+    return plan_run_rec(p, pose1, pose2, tol, max_iter, flags, alpha, contact, grad, iters, status, nullptr, stream);
 }
 
 int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* pose1, const double* pose2, double tol,
@@ -1074,17 +1117,35 @@ int dcol_comm_destroy(dcol_comm* c) {
 int dcol_prox_batch_multi_gpu(const dcol_plan* p, dcol_comm* c, const double* pose1, const double* pose2, double tol,
                               int32_t max_iter, int32_t flags, int64_t cap, double* alpha, double* grad,
                               int32_t* iters, int32_t* status, double* rec_local, double* rec_all, void* stream) {
-    if (!p || !c || !alpha || !iters || !status || !rec_local || !rec_all)
+    if (!p || !c || !rec_all || (rec_local && (!alpha || !iters || !status)))
         return fail(DCOL_ERR_ARG, "dcol_prox_batch_multi_gpu: NULL argument");
     if (cap < p->B) return fail(DCOL_ERR_ARG, "dcol_prox_batch_multi_gpu: cap < shard size");
     if (p->table->device != c->device)
         return fail(DCOL_ERR_ARG, "dcol_prox_batch_multi_gpu: plan and communicator on different devices");
     const int32_t rflags = flags & ~DCOL_CONTACT;   // the record carries no contact point
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (!rec_local) {
+        // in place: the solver epilogues write this rank's records straight into its slice of
+        // rec_all (no pack pass, no local copy inside the all-gather); rows past the shard
+        // are all-ones bytes (NaN doubles, int pair (-1, -1))
+        double* mine = rec_all + (size_t)c->rank * (size_t)cap * DCOL_REC;
+        int rc = plan_run_rec(p, pose1, pose2, tol, max_iter, rflags, alpha, nullptr,
+                              (rflags & DCOL_GRAD_ANY) ? grad : nullptr, iters, status, mine, stream);
+        if (rc != DCOL_SUCCESS) return rc;
+        DeviceGuard g(c->device);
+        if (cap > p->B) {
+            const hipError_t e = hipMemsetAsync(mine + (size_t)p->B * DCOL_REC, 0xFF,
+                                                (size_t)(cap - p->B) * DCOL_REC * sizeof(double), st);
+            if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("record tail: ") + hipGetErrorString(e));
+        }
+        ncclResult_t r = rccl().all_gather(mine, rec_all, (size_t)cap * DCOL_REC, ncclDouble, c->comm, st);
+        if (r != ncclSuccess) return fail(DCOL_ERR_HIP, "ncclAllGather: " + rccl_error(r));
+        return DCOL_SUCCESS;
+    }
     int rc = dcol_plan_run(p, pose1, pose2, tol, max_iter, rflags, alpha, nullptr,
                            (rflags & DCOL_GRAD_ANY) ? grad : nullptr, iters, status, stream);
     if (rc != DCOL_SUCCESS) return rc;
     DeviceGuard g(c->device);
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const bool want_grad = (rflags & DCOL_GRAD_ANY) && grad;
     if (cap > 0) {
         const int64_t grid = (cap + kPackRows - 1) / kPackRows;

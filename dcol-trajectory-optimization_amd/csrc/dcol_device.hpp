@@ -132,6 +132,20 @@ struct DevRow {
 };
 static_assert(sizeof(DevRow) == 64, "DevRow layout");
 
+constexpr int kRec = 14;   // doubles per packed record (include/dcol.h DCOL_REC)
+
+// the record's last slot: (int32 status, int32 iters) in one 8-byte word (status low)
+DCOL_HD double rec_ints(int32_t status, int32_t iters) {
+    const unsigned long long w = ((unsigned long long)(unsigned)iters << 32) | (unsigned long long)(unsigned)status;
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __longlong_as_double((long long)w);
+#else
+    double d;
+    __builtin_memcpy(&d, &w, sizeof d);
+    return d;
+#endif
+}
+
 struct KArgs {
     const DevShape* __restrict__ shapes;
     const DevRow* __restrict__ rows;
@@ -151,6 +165,11 @@ struct KArgs {
     double* __restrict__ grad;          // [12][B]
     int32_t* __restrict__ iters;        // [B]
     int32_t* __restrict__ status;       // [B]
+    // [B][kRec] packed per-pair records (include/dcol.h DCOL_REC: alpha, grad(12), the int32
+    // pair (status, iters) in the last slot), written straight from the solver's epilogue by
+    // dcol_prox_batch_multi_gpu's in-place path; nullptr: none.  With rec set, alpha / grad /
+    // iters / status may be nullptr (record-only).
+    double* __restrict__ rec = nullptr;
     // Suspend / resume (variants with FL bit 4; dcol_capi.cpp): in the main launch, a wave
     // whose still-iterating pairs drop to susp_t or fewer, at iteration susp_min or later,
     // hands those pairs -- their iterate (x, s, z, r) and iteration count -- to the resume
@@ -1920,7 +1939,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1) {
     const double nan = __builtin_nan("");
     const bool ok = st == ST_OK;
     double g[12];
-    const bool want_grad = (A.flags & (F_GRAD_FD | F_GRAD_ENV | F_GRAD_IMP)) && A.grad;
+    const bool want_grad = (A.flags & (F_GRAD_FD | F_GRAD_ENV | F_GRAD_IMP)) && (A.grad || A.rec);
     if (want_grad) {
         // Phase boundary: make the gradient re-read poses, shape records and row descriptors
         // instead of keeping the assembly-phase copies live across the whole PDIP loop
@@ -1991,28 +2010,47 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1) {
         }
     }
     DCOL_STAMP(A, pi, q, 5);
+    double* const rec = A.rec ? A.rec + (int64_t)kRec * pi : nullptr;
     if (want_grad) {
         if (LPP >= 2) {   // lane 1 of the group holds primitive 2's block (see above)
             if (q == 1) {
 #pragma unroll
-                for (int c = 0; c < 6; ++c) A.grad[(6 + c) * B + pi] = ok ? g[c] : nan;
+                for (int c = 0; c < 6; ++c) {
+                    const double v = ok ? g[c] : nan;
+                    if (A.grad) A.grad[(6 + c) * B + pi] = v;
+                    if (rec) rec[7 + c] = v;
+                }
             }
         } else {
 #pragma unroll
-            for (int c = 6; c < 12; ++c) A.grad[c * B + pi] = g[c];
+            for (int c = 6; c < 12; ++c) {
+                if (A.grad) A.grad[c * B + pi] = g[c];
+                if (rec) rec[1 + c] = g[c];
+            }
         }
     }
     if (q != 0) return;
-    A.alpha[pi] = ok ? P.x[3] : nan;
+    const double al = ok ? P.x[3] : nan;
+    if (A.alpha) A.alpha[pi] = al;
     if (A.iters) A.iters[pi] = it;
     if (A.status) A.status[pi] = st;
     if ((A.flags & F_CONTACT) && A.contact) {
 #pragma unroll
         for (int c = 0; c < 3; ++c) A.contact[c * B + pi] = ok ? P.x[c] : nan;
     }
-    if (want_grad) {
+    if (want_grad && A.grad) {
 #pragma unroll
         for (int c = 0; c < 6; ++c) A.grad[c * B + pi] = g[c];
+    }
+    if (rec) {   // the record's alpha, primitive 1's gradient (all 12 NaN without one), ints
+        rec[0] = al;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) rec[1 + c] = want_grad ? g[c] : nan;
+        if (!want_grad) {
+#pragma unroll
+            for (int c = 6; c < 12; ++c) rec[1 + c] = nan;
+        }
+        rec[13] = rec_ints(st, it);
     }
 }
 

@@ -134,11 +134,16 @@ class NativeComm:
         return bytes(buf)
 
     def solve_gather(self, plan, pose1, pose2, cap: int, tol=1e-6, max_iter=50, grad="fd", out=None,
-                     stream=None, rec_local=None, rec_all=None):
+                     stream=None, rec_local=None, rec_all=None, in_place=False, soa=True):
         """Solve this rank's shard (``plan`` over its pairs; torch float64 [6, n] poses on the
         device) and all-gather the packed records: returns (out, rec_all) with rec_all a
         torch float64 [world * cap, REC] tensor (rank r's shard at rows r * cap), asynchronous
-        on ``stream``.  Same record layout as :meth:`ShardedBatch.gather`."""
+        on ``stream``.  Same record layout as :meth:`ShardedBatch.gather`.
+
+        in_place: the kernels write the records straight into this rank's rows of rec_all and
+        the all-gather runs in place (include/dcol.h, rec_local == NULL); rows past the shard
+        are all-ones bytes (NaN, int pair (-1, -1)).  soa=False (in place only): no per-pair
+        output arrays, records only (out is returned as None)."""
         import ctypes
 
         import torch
@@ -160,22 +165,28 @@ class NativeComm:
         # all-gather still read it on `stream`, so its block may only be handed out again to
         # later work on that same stream (ordered after them).  rec_local / rec_all / out may
         # also be passed in (hot loops reuse them; then the caller owns their lifetime).
+        if in_place and rec_local is not None:
+            raise ValueError("in_place writes into rec_all: pass no rec_local")
+        if not soa and not in_place:
+            raise ValueError("soa=False needs in_place=True (the pack pass reads the per-pair arrays)")
         with torch.cuda.stream(stream):
-            if out is None:
+            if out is None and soa:
                 out = alloc_outputs(n, dev, bool(flags), False)
-            if rec_local is None:
+            if rec_local is None and not in_place:
                 rec_local = torch.empty((cap, REC), dtype=torch.float64, device=dev)
             if rec_all is None:
                 rec_all = torch.empty((self.world * cap, REC), dtype=torch.float64, device=dev)
-        for t, shape in ((rec_local, (cap, REC)), (rec_all, (self.world * cap, REC))):
+        bufs = [(rec_all, (self.world * cap, REC))] + ([] if in_place else [(rec_local, (cap, REC))])
+        for t, shape in bufs:
             if t.dtype != torch.float64 or tuple(t.shape) != shape or not t.is_contiguous() or t.device != dev:
                 raise ValueError(f"record buffers must be contiguous float64 {shape} on {dev}")
         ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        o = out if soa else {}
         _lib.check(_lib.load().dcol_prox_batch_multi_gpu(
             plan.handle, self.handle, ptr(pose1), ptr(pose2), float(tol), int(max_iter), flags, int(cap),
-            ptr(out["alpha"]), ptr(out.get("grad")), ptr(out["iters"]), ptr(out["status"]), ptr(rec_local),
+            ptr(o.get("alpha")), ptr(o.get("grad")), ptr(o.get("iters")), ptr(o.get("status")), ptr(rec_local),
             ptr(rec_all), ctypes.c_void_p(stream.cuda_stream)), "dcol_prox_batch_multi_gpu")
-        return out, rec_all
+        return (out if soa else None), rec_all
 
     def close(self):
         from . import _lib

@@ -205,7 +205,12 @@ int dcol_comm_destroy(dcol_comm* comm);
  * dcol_plan_run), pack row i of rec_local[cap][DCOL_REC] = [alpha, grad(12) (NaN without a
  * gradient flag), (int32 status, int32 iters)] (rows n..cap-1 = NaN), then all-gather every rank's
  * rec_local into rec_all[nranks * cap][DCOL_REC] (rank r's rows at r * cap).  Requires
- * n <= cap, the same cap on every rank.  Asynchronous on `stream`; no allocation.       */
+ * n <= cap, the same cap on every rank.  Asynchronous on `stream`; no allocation.
+ * rec_local == NULL: in place -- the solver kernels write the records straight into this
+ * rank's rows of rec_all (rows n..cap-1: all-ones bytes, i.e. NaN doubles and the int pair
+ * (-1, -1)) and the all-gather runs in place (sendbuff = rec_all + rank * cap * DCOL_REC):
+ * no pack pass and no local copy.  alpha / grad / iters / status are then optional (NULL:
+ * records only; given: filled as well).                                                  */
 int dcol_prox_batch_multi_gpu(const dcol_plan* plan, dcol_comm* comm, const double* pose1, const double* pose2,
                               double tol, int32_t max_iter, int32_t flags, int64_t cap, double* alpha,
                               double* grad, int32_t* iters, int32_t* status, double* rec_local,

@@ -172,6 +172,53 @@ def test_native_comm_multi_gpu_world1(engine):
     np.testing.assert_array_equal(u["status"], d["status"])
 
 
+@pytest.mark.parametrize("grad", ["fd", "envelope", None])
+@pytest.mark.parametrize("fuse", [True, False])
+def test_native_comm_in_place_records(engine, grad, fuse):
+    """In-place record path of dcol_prox_batch_multi_gpu (rec_local NULL): the solver
+    epilogues (and the reject kernel) write the records straight into the gathered buffer.
+    Records-only and with the per-pair arrays, fused and per-bucket plans, every gradient
+    mode: equal bitwise to the pack-pass path / the plan's own outputs; rows past the shard
+    all-ones bytes (NaN, int pair (-1, -1)); gradients NaN without a gradient flag."""
+    import torch
+    from dcol_amd.dist import REC, NativeComm, unpack
+    d = load_golden([p for p in golden_files() if p.endswith("synthetic_mixed.npz")][0])
+    s1, s2 = register(engine, d)
+    plan = engine.plan(s1, s2, fuse=fuse)
+    p1 = torch.from_numpy(np.ascontiguousarray(d["pose1"].T)).cuda()
+    p2 = torch.from_numpy(np.ascontiguousarray(d["pose2"].T)).cuda()
+    n = plan.B
+    comm = NativeComm(NativeComm.unique_id(), 1, 0, 0)
+    try:
+        _, packed = comm.solve_gather(plan, p1, p2, cap=n + 5, grad=grad)
+        junk = torch.full((n + 5, REC), 3.0, dtype=torch.float64, device="cuda")
+        none_out, rec_only = comm.solve_gather(plan, p1, p2, cap=n + 5, grad=grad, rec_all=junk.clone(),
+                                               in_place=True, soa=False)
+        out, rec_soa = comm.solve_gather(plan, p1, p2, cap=n + 5, grad=grad, rec_all=junk.clone(), in_place=True)
+        ref = plan.run(p1, p2, grad=grad or None, contact=False)
+        torch.cuda.synchronize()
+    finally:
+        comm.close()
+    assert none_out is None
+    packed = packed.cpu().numpy()
+    for rec in (rec_only.cpu().numpy(), rec_soa.cpu().numpy()):
+        assert rec.shape == (n + 5, REC)
+        assert np.all(rec[n:].view(np.uint64) == np.uint64(0xFFFFFFFFFFFFFFFF))
+        np.testing.assert_array_equal(rec[:n].view(np.uint64), packed[:n].view(np.uint64))
+        u = unpack(rec[:n])
+        np.testing.assert_array_equal(u["alpha"], ref["alpha"].cpu().numpy())
+        np.testing.assert_array_equal(u["status"], ref["status"].cpu().numpy())
+        np.testing.assert_array_equal(u["iters"], ref["iters"].cpu().numpy())
+        if grad is None:
+            assert np.all(np.isnan(u["grad"]))
+        else:
+            np.testing.assert_array_equal(u["grad"], ref["grad"].cpu().numpy().T)
+    np.testing.assert_array_equal(out["alpha"].cpu().numpy(), ref["alpha"].cpu().numpy())
+    np.testing.assert_array_equal(out["iters"].cpu().numpy(), ref["iters"].cpu().numpy())
+    assert (d["status"] != 0).any()   # the golden set's unsupported pairs: records from the reject kernel
+    np.testing.assert_array_equal(unpack(rec_only.cpu().numpy()[:n])["status"], d["status"])
+
+
 def test_native_comm_side_stream(engine):
     """dcol_prox_batch_multi_gpu on a non-default stream with the buffers allocated by
     NativeComm.solve_gather (they belong to that stream in torch's allocator): the records
