@@ -38,7 +38,7 @@ CATS = [("fp64", re.compile(r"^v_(fma|mul|add|fmac|rcp|rsq|sqrt|max|min|ldexp|di
         ("valu", re.compile(r"^v_"))]
 
 
-def stats(spec, waves):
+def stats(spec, waves, extra=()):
     parts = [int(v) for v in spec.split(":")]
     n, s, o, l = parts[:4]
     oe = parts[4] if len(parts) > 4 else 0
@@ -49,7 +49,7 @@ def stats(spec, waves):
         open(src, "w").write(SRC.format(n=n, s=s, o=o, l=l, oe=oe, w=waves, full="true" if fl & 1 else "false",
                                         ball="true" if fl & 2 else "false", cone="true" if fl & 4 else "false"))
         r = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=on", f"-I{CSRC}",
-                            "-S", "--offload-device-only", src, "-o", asm], capture_output=True, text=True)
+                            *extra, "-S", "--offload-device-only", src, "-o", asm], capture_output=True, text=True)
         if r.returncode:
             sys.exit(r.stderr)
         lines = open(asm).read().splitlines()
@@ -98,9 +98,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("specs", nargs="+")
     ap.add_argument("--waves", type=int, default=1)
+    ap.add_argument("--flags", default="-mllvm -amdgpu-sched-strategy=max-ilp",
+                    help="extra compiler flags (default: the library's, csrc/Makefile)")
     args = ap.parse_args()
     for sp in args.specs:
-        print(stats(sp, args.waves), flush=True)
+        print(stats(sp, args.waves, args.flags.split()), flush=True)
 
 
 if __name__ == "__main__":
