@@ -98,8 +98,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("specs", nargs="+")
     ap.add_argument("--waves", type=int, default=1)
-    ap.add_argument("--flags", default="-mllvm -amdgpu-sched-strategy=max-ilp",
-                    help="extra compiler flags (default: the library's, csrc/Makefile)")
+    ap.add_argument("--flags", default="",
+                    help="extra compiler flags (default none, as the library's build; the codegen-invariance "
+                         "twin lib_xcheck adds -mllvm -amdgpu-sched-strategy=max-ilp)")
     args = ap.parse_args()
     for sp in args.specs:
         print(stats(sp, args.waves, args.flags.split()), flush=True)
