@@ -150,6 +150,10 @@ class NativeComm:
 
         from . import _lib
         from .engine import alloc_outputs, grad_flag
+        if in_place and rec_local is not None:
+            raise ValueError("in_place writes into rec_all: pass no rec_local")
+        if not soa and not in_place:
+            raise ValueError("soa=False needs in_place=True (the pack pass reads the per-pair arrays)")
         n = plan.B
         dev = torch.device("cuda", self.device)
         for t in (pose1, pose2):
@@ -165,10 +169,6 @@ class NativeComm:
         # all-gather still read it on `stream`, so its block may only be handed out again to
         # later work on that same stream (ordered after them).  rec_local / rec_all / out may
         # also be passed in (hot loops reuse them; then the caller owns their lifetime).
-        if in_place and rec_local is not None:
-            raise ValueError("in_place writes into rec_all: pass no rec_local")
-        if not soa and not in_place:
-            raise ValueError("soa=False needs in_place=True (the pack pass reads the per-pair arrays)")
         with torch.cuda.stream(stream):
             if out is None and soa:
                 out = alloc_outputs(n, dev, bool(flags), False)

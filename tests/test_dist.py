@@ -179,3 +179,18 @@ def test_native_comm_setup_never_splits_collectives(fail):
         assert "librccl" in res[0][3] and "rank 0" in res[1][3]
     else:   # the caller's all-reduce of the outcome then makes rank 0 drop its communicator
         assert res[0][1] and not res[1][1] and "stand-in" in res[1][3]
+
+
+def test_native_comm_solve_gather_argument_combinations():
+    """NativeComm.solve_gather refuses the combinations the C-ABI cannot honour, before any
+    device work: in place with a rec_local, or records-only (soa=False) with the pack pass."""
+    from dcol_amd.dist import NativeComm
+    comm = object.__new__(NativeComm)          # no communicator: the checks come first
+    comm.world, comm.rank, comm.device, comm.handle = 1, 0, 0, None
+
+    class _Plan:
+        B = 4
+    with pytest.raises(ValueError, match="in_place"):
+        comm.solve_gather(_Plan(), None, None, 4, rec_local=object(), in_place=True)
+    with pytest.raises(ValueError, match="soa=False"):
+        comm.solve_gather(_Plan(), None, None, 4, soa=False)

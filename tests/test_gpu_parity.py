@@ -219,6 +219,33 @@ def test_native_comm_in_place_records(engine, grad, fuse):
     np.testing.assert_array_equal(unpack(rec_only.cpu().numpy()[:n])["status"], d["status"])
 
 
+def test_native_comm_in_place_edge_shapes(engine):
+    """In-place records with no tail rows (cap == n) and for an empty shard (every row of
+    the rank's slice is tail: all-ones bytes)."""
+    import torch
+    from dcol_amd.dist import NativeComm, unpack
+    d = load_golden([p for p in golden_files() if p.endswith("synthetic_polypoly.npz")][0])
+    s1, s2 = register(engine, d)
+    plan = engine.plan(s1[:300], s2[:300])
+    p1 = torch.from_numpy(np.ascontiguousarray(d["pose1"][:300].T)).cuda()
+    p2 = torch.from_numpy(np.ascontiguousarray(d["pose2"][:300].T)).cuda()
+    empty = engine.plan(s1[:0], s2[:0])
+    e1 = torch.zeros((6, 0), dtype=torch.float64, device="cuda")
+    comm = NativeComm(NativeComm.unique_id(), 1, 0, 0)
+    try:
+        _, rec = comm.solve_gather(plan, p1, p2, cap=300, grad="fd", in_place=True, soa=False)
+        _, rec0 = comm.solve_gather(empty, e1, e1.clone(), cap=3, grad="fd", in_place=True, soa=False)
+        ref = plan.run(p1, p2, grad="fd", contact=False)
+        torch.cuda.synchronize()
+    finally:
+        comm.close()
+    u = unpack(rec.cpu().numpy())
+    np.testing.assert_array_equal(u["alpha"], ref["alpha"].cpu().numpy())
+    np.testing.assert_array_equal(u["grad"], ref["grad"].cpu().numpy().T)
+    np.testing.assert_array_equal(u["iters"], ref["iters"].cpu().numpy())
+    assert np.all(rec0.cpu().numpy().view(np.uint64) == np.uint64(0xFFFFFFFFFFFFFFFF))
+
+
 def test_native_comm_side_stream(engine):
     """dcol_prox_batch_multi_gpu on a non-default stream with the buffers allocated by
     NativeComm.solve_gather (they belong to that stream in torch's allocator): the records
