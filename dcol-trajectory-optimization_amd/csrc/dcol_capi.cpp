@@ -237,6 +237,7 @@ int dcol_table_create(const dcol_shape_desc* shapes, int32_t n, int32_t device, 
             (void)hipGetLastError();
     }
     t->shapes.resize(n);
+    init_row_pool(t->rows);
     for (int32_t i = 0; i < n; ++i) {
         int rc = digest_shape(shapes[i], i, t->shapes[i], t->rows);
         if (rc != DCOL_SUCCESS) {
@@ -244,7 +245,6 @@ int dcol_table_create(const dcol_shape_desc* shapes, int32_t n, int32_t device, 
             return rc;
         }
     }
-    if (t->rows.empty()) t->rows.resize(1);   // keep a valid device pointer
     if (t->shapes.empty()) t->shapes.resize(1);
     DeviceGuard g(device);
     hipError_t e = hipMalloc(&t->d_shapes, sizeof(DevShape) * t->shapes.size());

@@ -244,11 +244,12 @@ DCOL_HD void dcm_from_mrp(double p1, double p2, double p3, double Q[9]) {
 // problem_matrices.py:275-282 (r_eff = r + Q r_offset; Q_eff = Q Q_offset).  With
 // identity offsets (S.plain) the products are exact no-ops (q*1 + q'*0 + q''*0 == q,
 // r + (+-0) == r) and are skipped: same bits, ~36 fewer instructions per frame.
-DCOL_HD void make_frame(const DevShape& S, const double th[6], Frame& F) {
+// plain: S.plain, passed in by a caller that loaded it early (see solve_one)
+DCOL_HD void make_frame(const DevShape& S, const double th[6], Frame& F, int32_t plain) {
     double Q[9];
     dcm_from_mrp(th[3], th[4], th[5], Q);
     double qe[9], qr[3];
-    if (S.plain) {
+    if (plain) {
 #pragma unroll
         for (int k = 0; k < 9; ++k) qe[k] = Q[k];
 #pragma unroll
@@ -271,6 +272,7 @@ DCOL_HD void make_frame(const DevShape& S, const double th[6], Frame& F) {
         F.re[k] = th[k] + qr[k];
     }
 }
+DCOL_HD void make_frame(const DevShape& S, const double th[6], Frame& F) { make_frame(S, th, F, S.plain); }
 
 // ------------------------------------------------------------------------------------
 // closed-form envelope gradient
@@ -675,13 +677,13 @@ struct Solver {
 
     // -------- assembly (problem_matrices.py + combine_problem_matrices.py) --------------
     // One orthant slot: row i = k * LPP + q of primitive p2 (frame F) -> G[k], h in r[k].
+    // A slot without a row (v false) reads the pool's zero row 0 (dcol_host.hpp
+    // init_row_pool) instead of skipping its loads: a load under a per-slot branch waits for
+    // its data before the branch joins, which serialised the slots' L2 round trips.
     DCOL_HD void orth_row(const double* __restrict__ rows, int k, bool v, bool p2, int ri, const Frame& F) {
-        double a0 = 0, a1 = 0, a2 = 0, g3 = 0, e0 = 0, e1 = 0;
-        if (v) {
-            const double2* rw = reinterpret_cast<const double2*>(rows + 8 * (int64_t)ri);
-            const double2 q0 = rw[0], q1 = rw[1], q2 = rw[2];
-            a0 = q0.x; a1 = q0.y; a2 = q1.x; g3 = q1.y; e0 = q2.x; e1 = q2.y;
-        }
+        const double2* rw = reinterpret_cast<const double2*>(rows + 8 * (int64_t)(v ? ri : 0));
+        const double2 q0 = rw[0], q1 = rw[1], q2 = rw[2];
+        const double a0 = q0.x, a1 = q0.y, a2 = q1.x, g3 = q1.y, e0 = q2.x, e1 = q2.y;
         const double u0 = F.Qe[0] * a0 + F.Qe[1] * a1 + F.Qe[2] * a2;
         const double u1 = F.Qe[3] * a0 + F.Qe[4] * a1 + F.Qe[5] * a2;
         const double u2 = F.Qe[6] * a0 + F.Qe[7] * a1 + F.Qe[8] * a2;
@@ -694,12 +696,9 @@ struct Solver {
     }
     // PART: one extra-column slot (pose-independent row [0 0 0, g3, ex], h = 0)
     DCOL_HD void ext_row(const double* __restrict__ rows, int k, bool v, int ri) {
-        double g3 = 0, e0 = 0, e1 = 0;
-        if (v) {
-            const double2* rw = reinterpret_cast<const double2*>(rows + 8 * (int64_t)ri);
-            const double2 q1 = rw[1], q2 = rw[2];
-            g3 = q1.y; e0 = q2.x; e1 = q2.y;
-        }
+        const double2* rw = reinterpret_cast<const double2*>(rows + 8 * (int64_t)(v ? ri : 0));
+        const double2 q1 = rw[1], q2 = rw[2];
+        const double g3 = q1.y, e0 = q2.x, e1 = q2.y;
         G[k][3] = g3;
 #pragma unroll
         for (int j = 4; j < N; ++j) G[k][j] = excol(j, 0, e0, e1);
@@ -1909,8 +1908,11 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1) {
         th2[c] = A.pose2[c * B + pi];
     }
     Frame F1, F2;
-    make_frame(S1, th1, F1);
-    make_frame(S2, th2, F2);
+    // both records' plain flags read before either frame: their loads issue together (read
+    // inside make_frame, the second record's load waited for the first frame's branch)
+    const int32_t plain1 = S1.plain, plain2 = S2.plain;
+    make_frame(S1, th1, F1, plain1);
+    make_frame(S2, th2, F2, plain2);
     DCOL_STAMP(A, pi, q, 1);
 
     Solver<N, NSOC, OMAX, LPP, BALL, CONE, OE> P;

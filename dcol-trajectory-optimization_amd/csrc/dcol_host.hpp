@@ -83,6 +83,11 @@ inline int choose_lpp(int N, int nsoc, int omax, int fl = 0) {
     return (first == 0 && fl != 0) ? choose_lpp(N, nsoc, omax, 0) : first;   // no copies of the flavour: dense
 }
 
+// A row pool starts with one zero row (index 0; every shape's rows follow): a lane slot
+// without a row of its pair loads that row instead of branching around its loads (the
+// kernels' orth_row / ext_row), so all slots' loads issue back to back.
+inline void init_row_pool(std::vector<DevRow>& rows) { rows.assign(1, DevRow{}); }
+
 // Static digest of one primitive (misc_primitive_constructor.py:4-88 ->
 // problem_matrices.py:4-209).  Every orthant row is [Qe a, g3, ex0, ex1] with
 // h = (Qe a) . r_eff; the SOC block is generated in-kernel from (kind, R, cone_c, tanb).

@@ -15,11 +15,11 @@ extern "C" int dcol_emul_batch(const dcol_shape_desc* shapes, int32_t n, int64_t
                                int32_t* iters, int32_t* status) {
     std::vector<DevShape> sh(n);
     std::vector<DevRow> rows;
+    init_row_pool(rows);
     for (int32_t i = 0; i < n; ++i) {
         int rc = digest_shape(shapes[i], i, sh[i], rows);
         if (rc) return rc;
     }
-    if (rows.empty()) rows.resize(1);
     std::vector<double> p1(6 * B), p2(6 * B), ct(3 * B), gr(12 * B);
     for (int64_t i = 0; i < B; ++i)
         for (int q = 0; q < 6; ++q) {

@@ -221,7 +221,7 @@ def test_structured_cone_rows_equal_dense(tmp_path):
 @pytest.mark.skipif(not os.path.exists(XCHECK_LIB), reason="lib_xcheck not built (make -C csrc xcheck)")
 def test_codegen_invariance_mixed(tmp_path):
     """The product library and its twin built from the same sources with another machine
-    schedule (-amdgpu-sched-strategy=max-ilp; Makefile target xcheck) must agree BITWISE on
+    schedule (each unit under the other of default / max-ilp; Makefile target xcheck) must agree BITWISE on
     the whole 1M mixed workload (every throughput variant of configs[4], both gradient
     modes, contact points): FP semantics are fixed in the IR before scheduling, so any
     difference is a machine-code defect -- the class of fault that made the 326f844 build

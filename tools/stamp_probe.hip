@@ -53,6 +53,7 @@ int main(int argc, char** argv) {
     }
     std::vector<DevShape> sh(NS);
     std::vector<DevRow> rows;
+    init_row_pool(rows);
     for (int k = 0; k < NS; ++k) digest_shape(descs[k], k, sh[k], rows);
     std::vector<int32_t> s1(B), s2(B);
     std::vector<double> p1(6 * B), p2(6 * B);
