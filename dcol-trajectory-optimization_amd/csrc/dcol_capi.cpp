@@ -347,8 +347,15 @@ void latency_config(Launch& L) {
 // fused_part: a row-partitioned bucket is used only where the fused small-plan kernel has
 // its case (the retry of a small plan that would otherwise lose its single fused launch;
 // the other pairs take the dense-row kernels, which the fused kernel covers)
+// lat_part: a row-partitioned bucket compiled only for one lane per pair is not used (the
+// retry of a plan that cannot fill the GPU: one lane working through every row of the pair
+// is slower than the dense rows' multi-lane groups -- polygon x box, 1,000 pairs: 84 us in
+// the (11, 5) one-lane bucket against 52 us in the dense (6, 1, 12) four-lane kernel)
+// small_out: set to whether the plan cannot fill the GPU (its buckets took their latency
+// configurations)
 int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, dcol_plan* p,
-                 std::vector<int32_t>& perm, bool case4, bool fused_part = false) {
+                 std::vector<int32_t>& perm, bool case4, bool fused_part = false, bool lat_part = false,
+                 bool* small_out = nullptr) {
     const int32_t ns = (int32_t)t->shapes.size();
     // kind, N, nsoc, omax, lpp, ball (SOC blocks all balls: no cone), code, oe (row partition)
     using Key = std::tuple<int, int, int, int, int, int, int, int>;
@@ -370,6 +377,8 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
         if (fused_part && c.status == DCOL_OK && c.oe > 0 &&
             fused_vid(c.N, c.nsoc, c.omax, part_lpp(c.N, c.nsoc, c.omax, c.oe, true),
                       (none_cone && !ball_disabled()) ? LF_BALL : 0, c.oe) < 0)
+            c = classify(a, b, case4, false);
+        if (lat_part && c.status == DCOL_OK && c.oe > 0 && part_lpp(c.N, c.nsoc, c.omax, c.oe, true) < 2)
             c = classify(a, b, case4, false);
         const int ball = c.nsoc == 0 ? 0
                          : (none_cone && !ball_disabled()) ? 1
@@ -420,6 +429,7 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
     for (const Group& G : groups)
         if (std::get<0>(G.key) == 0) plan_lanes += G.n * std::get<4>(G.key);
     const bool small_plan = plan_lanes < 64LL * t->simds;
+    if (small_out) *small_out = small_plan;
     int64_t at = 0;
     for (auto& kv : gid_of_key) {   // key order
         Group& G = groups[kv.second];
@@ -581,10 +591,19 @@ int plan_fuse(const dcol_table* t, dcol_plan* p, bool allow) {
 // buckets one by one)
 int bucket_and_fuse(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, dcol_plan* p,
                     std::vector<int32_t>& perm, bool case4, bool allow_fuse) {
-    int rc = bucket_pairs(t, B, s1, s2, p, perm, case4);
+    bool small = false;
+    int rc = bucket_pairs(t, B, s1, s2, p, perm, case4, false, false, &small);
     if (rc != DCOL_SUCCESS) return rc;
+    // a plan that cannot fill the GPU: no one-lane row-partitioned buckets (bucket_pairs)
+    bool lat_part = false;
+    if (small && !lpp_forced())
+        for (const Launch& L : p->launches) lat_part = lat_part || (L.kind == 0 && L.oe > 0 && L.lpp < 2);
+    if (lat_part) {
+        rc = bucket_pairs(t, B, s1, s2, p, perm, case4, false, true);
+        if (rc != DCOL_SUCCESS) return rc;
+    }
     if (plan_fuse(t, p, true) == 2) {
-        rc = bucket_pairs(t, B, s1, s2, p, perm, case4, true);
+        rc = bucket_pairs(t, B, s1, s2, p, perm, case4, true, lat_part);
         if (rc != DCOL_SUCCESS) return rc;
         plan_fuse(t, p, true);
     }

@@ -195,8 +195,20 @@ struct KArgs {
         __builtin_amdgcn_sched_barrier(0);                                              \
         if ((q) == 0) (A).stamps[16 * (pi) + (k)] = t_;                                 \
     } while (0)
-// sub-phases of PDIP iteration 2 into stamps[16 * pi + 8 + k] (Solver::dbg)
-#define DCOL_ISTAMP(it, k)                                                              \
+// sub-phases of PDIP iteration 2 into stamps[16 * pi + 8 + k] (Solver::dbg); with
+// DCOL_STAMPS_INIT the sub-phases of initialize() instead (DCOL_NSTAMP)
+#ifdef DCOL_STAMPS_INIT
+#define DCOL_ISTAMP(it, k) \
+    do {                   \
+    } while (0)
+#define DCOL_NSTAMP(k) DCOL_ISTAMP_(2, k)
+#else
+#define DCOL_ISTAMP(it, k) DCOL_ISTAMP_(it, k)
+#define DCOL_NSTAMP(k) \
+    do {               \
+    } while (0)
+#endif
+#define DCOL_ISTAMP_(it, k)                                                             \
     do {                                                                                \
         if ((it) == 2 && dbg) {                                                         \
             __builtin_amdgcn_sched_barrier(0);                                          \
@@ -212,6 +224,9 @@ struct KArgs {
     } while (0)
 #define DCOL_ISTAMP(it, k) \
     do {                   \
+    } while (0)
+#define DCOL_NSTAMP(k) \
+    do {               \
     } while (0)
 #endif
 
@@ -1108,6 +1123,7 @@ struct Solver {
 
     // -------- initialize, pdip.py:291-332 ------------------------------------------------
     DCOL_HD bool initialize() {
+        DCOL_NSTAMP(0);
         double H[N][N], F[N][N], idg[N], gth[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) {
@@ -1165,15 +1181,19 @@ struct Solver {
         }
         allsum_sym(H);
         allsum_vec(gth);
+        DCOL_NSTAMP(1);
         const bool ok = chol(H, F, idg);             // F' = np.linalg.cholesky(G'G)
         chol_solve(F, idg, gth, x);                  // x_hat = L^-T L^-1 G'h
+        DCOL_NSTAMP(2);
         double t[M];
 #pragma unroll
         for (int k = 0; k < M; ++k) {
             r[k] = rowdot(k, x) - r[k];              // r = G x_hat - h  (quirk Q2: s~ = G x_hat - h)
             t[k] = r[k];
         }
+        DCOL_NSTAMP(3);
         bring2cone(t);
+        DCOL_NSTAMP(4);
         // quirk Q1: y = solve_triangular(L, -c) with lower=False reads diag(L) only:
         // y = -e_3 / L_33, then x = L^-T y
         double xz[N];
@@ -1187,7 +1207,9 @@ struct Solver {
         double zt[M];
 #pragma unroll
         for (int k = 0; k < M; ++k) zt[k] = rowdot(k, xz);
+        DCOL_NSTAMP(5);
         bring2cone(zt);
+        DCOL_NSTAMP(6);
 #pragma unroll
         for (int k = 0; k < M; ++k) {
             const bool v = vrow(k);
@@ -1195,6 +1217,7 @@ struct Solver {
             s[k] = v ? t[k] : one;
             z[k] = v ? zt[k] : one;
         }
+        DCOL_NSTAMP(7);
         return ok;
     }
 

@@ -7,6 +7,10 @@ For every ordered kind pair of the mixed workload (27 supported ones), B pairs o
 class are solved with FD gradients; prints per class the variant launched, pair-solves/s,
 kernel ms and mean / max Newton iterations.  Also times a latency-size batch (default 1,000
 pairs) per class.
+Each class line also carries its FP64 roofline fraction: the reference's COUNTED flops per
+pair (profiles/flop_model.json, oracle/dcol_oracle_opcount.cpp: assembly + pdip_fixed +
+pdip_per_iter x the batch's measured mean iterations + FD gradient) x pairs / kernel time,
+against the 78.6 TF/s FP64 vector peak (MI355X_MICROARCH.md).
 Usage: python3 tools/class_bench.py [--pairs 200000] [--small 1000 (0: skip)] [--reps 10] [--classes a-b,...]
 """
 import argparse
@@ -23,6 +27,7 @@ sys.path.insert(0, os.path.join(REPO, "dcol-trajectory-optimization_amd"))
 
 import bench  # noqa: E402
 
+FP64_PEAK = 78.6e12
 NAMES = {0: "polytope", 1: "sphere", 2: "cone", 3: "capsule", 4: "cylinder", 5: "polygon"}
 
 
@@ -41,6 +46,7 @@ def main():
     ids = np.array([eng.register(spec_from_arrays(tab, k)) for k in range(len(tab["type"]))], np.int32)
     by_kind = {k: np.flatnonzero(tab["type"] == k) for k in bench.MIXED_KINDS}
     combos = [(a, b) for a in bench.MIXED_KINDS for b in bench.MIXED_KINDS if a <= 2 or b <= 2]
+    fm = json.load(open(os.path.join(REPO, "profiles", "flop_model.json")))["classes"]
     rng = np.random.default_rng(0)
     stream = torch.cuda.current_stream(dev)
     rows = []
@@ -75,6 +81,11 @@ def main():
             rec[label] = {"pairs": B, "kernel_ms": round(ms, 4), "pair_solves_per_s": B / (ms * 1e-3),
                           "iters_mean": round(float(it[st == 0].mean()), 2), "iters_max": int(it.max()),
                           "ok_frac": float(np.mean(st == 0)), "launches": plan.num_launches}
+            m = fm.get(rec["class"])
+            if m:   # counted flops at this batch's mean iteration count
+                fl = m["assembly"] + m["pdip_fixed"] + m["pdip_per_iter"] * float(it[st == 0].mean()) + m["grad_fd"]
+                rec[label]["flops_per_pair"] = round(fl, 1)
+                rec[label]["fp64_roofline_frac"] = round(fl * B / (ms * 1e-3) / FP64_PEAK, 4)
         rows.append(rec)
         print(json.dumps(rec), flush=True)
     tot_big = sum(r["big"]["pairs"] / r["big"]["pair_solves_per_s"] for r in rows)

@@ -4,6 +4,7 @@
 //   hipcc -DDCOL_STAMPS --offload-arch=gfx950 -O3 -std=c++17 \
 //         -I dcol-trajectory-optimization_amd/csrc tools/stamp_probe.hip -o /tmp/stamp_probe
 //   /tmp/stamp_probe [pairs=100000] [flags=1 (FD) | 2 (envelope)]
+// (-DDCOL_STAMPS_INIT: sub-phases of initialize() in place of PDIP iteration 2's)
 // Prints mean cycles per phase (per pair group, lane 0's s_memtime) and the per-wave
 // (32 pairs) critical phase lengths.
 #include <hip/hip_runtime.h>
@@ -130,9 +131,15 @@ int main(int argc, char** argv) {
                 it_wmax / nw);
     for (int k = 0; k < 5; ++k)
         std::printf("  %-14s mean %9.0f cyc/pair   per-wave max %9.0f cyc\n", names[k], sum[k] / B, wmax[k] / nw);
-    // sub-phases of PDIP iteration 2 (pairs that reached it)
+    // sub-phases of PDIP iteration 2 (pairs that reached it), or with -DDCOL_STAMPS_INIT of
+    // initialize()
+#ifdef DCOL_STAMPS_INIT
+    const char* sub[7] = {"G'G, G'h + sums", "chol + solve", "r = G x - h", "bring2cone(s)",
+                          "L^-T y, G x_z", "bring2cone(z)", "s, z select"};
+#else
     const char* sub[7] = {"NT + normal matrix", "Cholesky", "predictor + bound", "rho, sigma, cp",
                           "corrector rhs", "corrector bound", "update"};
+#endif
     double ss[7] = {0};
     int64_t cnt = 0;
     for (int64_t i = 0; i < B; ++i) {
@@ -141,7 +148,11 @@ int main(int argc, char** argv) {
         ++cnt;
         for (int k = 0; k < 7; ++k) ss[k] += (double)(t[k + 1] - t[k]);
     }
+#ifdef DCOL_STAMPS_INIT
+    std::printf("  initialize (%lld pairs):\n", (long long)cnt);
+#else
     std::printf("  iteration 2 (%lld pairs):\n", (long long)cnt);
+#endif
     for (int k = 0; k < 7; ++k) std::printf("    %-20s %8.0f cyc\n", sub[k], cnt ? ss[k] / cnt : 0.0);
     return 0;
 }
