@@ -1037,31 +1037,53 @@ struct Solver {
                     for (int c = j; c < N; ++c) Hm[j][c] += gt[e][j] * gt[e][c];
         }
     }
-    // upper Cholesky H = F'F (scipy.linalg.cholesky); false if a pivot is <= 0, infinite or
-    // NaN.  Any non-finite entry of H's upper triangle makes some pivot non-finite (a
-    // diagonal entry directly, an off-diagonal one through F[j][c]^2), so a non-finite H
-    // always fails here and the caller only classifies failures.
+    // Factorisation of the normal matrix (scipy.linalg.cholesky / cho_solve, pdip.py:434-436),
+    // in one of two forms with the same interface (F: strict upper triangle, idg: per-pivot
+    // scale), chosen per kernel at compile time (LDL):
+    //  * upper Cholesky H = F_c' F_c: F = F_c, idg = 1 / diag(F_c) (v_rsq_f64 + refinement);
+    //  * square-root-free H = U' D U (U unit upper, D = diag(d), d_j = F_c[j][j]^2 -- the
+    //    same pivots): F = U, idg = 1 / d (v_rcp_f64 + one Newton step).  The pivots sit on
+    //    the replicated critical path of every PDIP iteration and of initialize(); without the
+    //    square-root refinement the poly x poly loop is 646 -> 614 instructions and its
+    //    Cholesky section 590 -> 476 cycles.  Used by the polytope x polytope kernels (NSOC
+    //    = 0).  The SOC kernels keep the square-root form: the factorisation's extra row
+    //    block (E below) pushed the one-wave N = 6 PART kernels into in-loop scratch (polygon
+    //    x polytope -13 %), and on the 1M mixed workload it moved one polytope x cone pair's
+    //    exit test (mu = tol (1 - 1e-7) in the oracle) across tol -- rounding-decided, but the
+    //    full-size tests hold every pair to the oracle's iteration count.
+    //    -DDCOL_CHOL_SQRT: the square-root form everywhere (A/B runs).
+    // False if a pivot is <= 0, infinite or NaN.  Any non-finite entry of H's upper triangle
+    // makes some pivot non-finite (a diagonal entry directly, an off-diagonal one through the
+    // products that update later pivots), so a non-finite H always fails here and the caller
+    // only classifies failures.
+#ifdef DCOL_CHOL_SQRT
+    static constexpr bool LDL = false;
+#else
+    static constexpr bool LDL = NSOC == 0;
+#endif
     DCOL_HD static bool chol(const double (&H)[N][N], double (&F)[N][N], double (&idg)[N]) {
         bool ok = true;
+        double E[LDL ? N : 1][N];   // LDL: E[k][c] = d_k U[k][c], the rows before their pivot's scaling
 #pragma unroll
         for (int j = 0; j < N; ++j) {
             double d = H[j][j];
 #pragma unroll
-            for (int k = 0; k < j; ++k) d -= F[k][j] * F[k][j];
+            for (int k = 0; k < j; ++k) d -= (LDL ? E[LDL ? k : 0][j] : F[k][j]) * F[k][j];
             ok = ok && pos_finite(d);
-            idg[j] = frsqrt(d);
-            F[j][j] = d * idg[j];
+            idg[j] = LDL ? frcp1(d) : frsqrt(d);
 #pragma unroll
             for (int c = j + 1; c < N; ++c) {
                 double t = H[j][c];
 #pragma unroll
-                for (int k = 0; k < j; ++k) t -= F[k][j] * F[k][c];
+                for (int k = 0; k < j; ++k) t -= (LDL ? E[LDL ? k : 0][j] : F[k][j]) * F[k][c];
+                if constexpr (LDL) E[j][c] = t;
                 F[j][c] = t * idg[j];
             }
         }
         return ok;
     }
-    // solve F'F x = b  (cho_solve((F, False), b))
+    // solve H x = b: Cholesky F_c' F_c x = b (cho_solve((F, False), b)); LDL forward U' y = b,
+    // w = y / d, backward U x = w
     DCOL_HD static void chol_solve(const double (&F)[N][N], const double (&idg)[N], const double* b, double* out) {
         double y[N];
 #pragma unroll
@@ -1069,14 +1091,25 @@ struct Solver {
             double t = b[j];
 #pragma unroll
             for (int k = 0; k < j; ++k) t -= F[k][j] * y[k];
-            y[j] = t * idg[j];
+            y[j] = LDL ? t : t * idg[j];
         }
 #pragma unroll
         for (int j = N - 1; j >= 0; --j) {
-            double t = y[j];
+            double t = LDL ? y[j] * idg[j] : y[j];
 #pragma unroll
             for (int k = j + 1; k < N; ++k) t -= F[j][k] * out[k];
-            out[j] = t * idg[j];
+            out[j] = LDL ? t : t * idg[j];
+        }
+    }
+    // quirk Q1 (pdip.py:313-318): y = solve_triangular(L, -c) with lower=False reads diag(L)
+    // only: y = -e_3 / L_33; then x = L^-T y, i.e. F_c x = y (LDL: U x = D^(-1/2) y = -e_3 / d_3)
+    DCOL_HD static void q1_solve(const double (&F)[N][N], const double (&idg)[N], double* out) {
+#pragma unroll
+        for (int j = N - 1; j >= 0; --j) {
+            double acc = (j == 3) ? -idg[3] : 0.0;
+#pragma unroll
+            for (int k = j + 1; k < N; ++k) acc -= F[j][k] * out[k];
+            out[j] = LDL ? acc : acc * idg[j];
         }
     }
     // group all-reduce of the packed upper triangle / of an N-vector
@@ -1197,13 +1230,7 @@ struct Solver {
         // quirk Q1: y = solve_triangular(L, -c) with lower=False reads diag(L) only:
         // y = -e_3 / L_33, then x = L^-T y
         double xz[N];
-#pragma unroll
-        for (int j = N - 1; j >= 0; --j) {
-            double acc = (j == 3) ? -idg[3] : 0.0;
-#pragma unroll
-            for (int k = j + 1; k < N; ++k) acc -= F[j][k] * xz[k];
-            xz[j] = acc * idg[j];
-        }
+        q1_solve(F, idg, xz);
         double zt[M];
 #pragma unroll
         for (int k = 0; k < M; ++k) zt[k] = rowdot(k, xz);
