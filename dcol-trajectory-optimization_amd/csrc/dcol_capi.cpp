@@ -724,6 +724,18 @@ int dcol_plan_num_buckets(const dcol_plan* p, int32_t* n) {
     return DCOL_SUCCESS;
 }
 
+int dcol_plan_bucket(const dcol_plan* p, int32_t i, int32_t info[8], int64_t* pairs) {
+    if (!p || !info || !pairs) return fail(DCOL_ERR_ARG, "dcol_plan_bucket: NULL argument");
+    if (i < 0 || i >= (int32_t)p->launches.size()) return fail(DCOL_ERR_ARG, "dcol_plan_bucket: index out of range");
+    const Launch& L = p->launches[(size_t)i];
+    const bool solve = L.kind == 0;
+    const int32_t v[8] = {L.kind, solve ? L.N : 0, solve ? L.nsoc : 0, solve ? L.omax : 0, solve ? L.lpp : 0,
+                          solve ? L.oe : 0, solve ? L.flags() : 0, solve ? 0 : L.code};
+    for (int k = 0; k < 8; ++k) info[k] = v[k];
+    *pairs = L.n;
+    return DCOL_SUCCESS;
+}
+
 }  // extern "C"
 
 namespace {

@@ -131,6 +131,22 @@ class Plan:
         _lib.check(lib.dcol_plan_num_buckets(h, ctypes.byref(n)), "dcol_plan_num_buckets")
         self.num_buckets = int(n.value)        # variant buckets (incl. rejected pairs)
 
+    def buckets(self) -> list:
+        """The plan's variant buckets (dcol_plan_bucket): one dict per bucket with kind
+        ("solve" / "reject"), N, nsoc, omax, lpp (lanes per pair of its launch), oe (extra-row
+        slots of a row-partitioned bucket, 0 for dense rows), flags (1 padding-free, 2 ball-SOC
+        rows, 4 cone-SOC rows), status (reject buckets) and pairs"""
+        lib = _lib.load()
+        info = (ctypes.c_int32 * 8)()
+        n = ctypes.c_int64()
+        out = []
+        for i in range(self.num_buckets):
+            _lib.check(lib.dcol_plan_bucket(self.handle, i, info, ctypes.byref(n)), "dcol_plan_bucket")
+            v = list(info)
+            out.append({"kind": "solve" if v[0] == 0 else "reject", "N": v[1], "nsoc": v[2], "omax": v[3],
+                        "lpp": v[4], "oe": v[5], "flags": v[6], "status": v[7], "pairs": int(n.value)})
+        return out
+
     def suspended(self) -> int:
         """pairs the last completed run handed to resume launches (synchronise first)"""
         n = ctypes.c_int64()

@@ -145,6 +145,13 @@ int dcol_plan_create_ex(const dcol_table* table, int64_t B, const int32_t* shape
 int dcol_plan_destroy(dcol_plan* plan);
 int dcol_plan_num_launches(const dcol_plan* plan, int32_t* n); /* kernel launches per run */
 int dcol_plan_num_buckets(const dcol_plan* plan, int32_t* n);  /* variant buckets (incl. rejects) */
+/* Bucket i (0 <= i < dcol_plan_num_buckets) of a plan, for tests and tools: info[0] kind (0 a
+ * solve bucket, 1 rejected pairs), [1] N (primal columns), [2] SOC blocks, [3] orthant-row
+ * bucket OMAX, [4] lanes per pair the launch runs at, [5] extra-column slots of a row-
+ * partitioned bucket (0: dense rows), [6] flags (1 padding-free, 2 ball-SOC rows, 4 cone-SOC
+ * rows), [7] the status of a reject bucket (else 0); *pairs = its pair count.  No reference
+ * counterpart (the plan is this library's own batching layer).                          */
+int dcol_plan_bucket(const dcol_plan* plan, int32_t i, int32_t info[8], int64_t* pairs);
 /* DCOL_PLAN_SUSPEND plans: pairs the last completed run handed to resume launches
  * (synchronous copy; call after the run's stream has been synchronised), else 0.       */
 int dcol_plan_suspended(const dcol_plan* plan, int64_t* n);

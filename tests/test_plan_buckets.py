@@ -1,0 +1,77 @@
+"""Plan bucketing through the C-ABI (dcol_plan_bucket): which kernel variant and lane
+configuration a plan launches -- the host logic of dcol_capi.cpp bucket_pairs /
+bucket_and_fuse.  Plans need a table on the device, so these run on the GPU box; no solve is
+launched."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _ids(engine, tab):
+    from dcol_amd import spec_from_arrays
+    return np.array([engine.register(spec_from_arrays(tab, k)) for k in range(len(tab["type"]))], np.int32)
+
+
+def _solves(plan):
+    return [b for b in plan.buckets() if b["kind"] == "solve"]
+
+
+def test_benchmark_batch_is_one_padding_free_two_lane_bucket(engine):
+    """configs[3] (100k random rectangular-prism pairs, bench.py): one bucket, the padding-free
+    (4, 0, 12) polytope x polytope kernel at two lanes per pair -- the kernel the roofline line
+    and the rocprofv3 summaries in profiles/ describe."""
+    import bench
+    tab = bench.shape_table(64, 0)
+    s1, s2 = bench.pairs(100_000, 64, 0)[:2]
+    ids = _ids(engine, tab)
+    plan = engine.plan(ids[s1], ids[s2], cache=False)
+    b = plan.buckets()
+    assert len(b) == 1 and plan.num_launches == 1
+    assert b[0] == {"kind": "solve", "N": 4, "nsoc": 0, "omax": 12, "lpp": 2, "oe": 0, "flags": 1, "status": 0,
+                    "pairs": 100_000}
+
+
+def _polygon_box(engine, B, seed=0):
+    import bench
+    tab = bench.mixed_table()
+    ids = _ids(engine, tab)
+    rng = np.random.default_rng(seed)
+    poly = np.flatnonzero(tab["type"] == 5)
+    box = np.flatnonzero(tab["type"] == 0)
+    s1 = rng.choice(poly, B).astype(np.int32)
+    s2 = rng.choice(box, B).astype(np.int32)
+    return engine.plan(ids[s1], ids[s2], cache=False)
+
+
+def test_large_polygon_box_plan_takes_the_row_partitioned_bucket(engine):
+    """A plan that fills the GPU runs pentagon x box pairs (5 edge rows + 6 faces) in the
+    row-partitioned (11, 5) bucket at its throughput configuration, one lane per pair."""
+    b = _solves(_polygon_box(engine, 200_000))
+    assert len(b) == 1
+    assert (b[0]["N"], b[0]["nsoc"], b[0]["omax"], b[0]["oe"], b[0]["lpp"]) == (6, 1, 11, 5, 1)
+
+
+@pytest.mark.parametrize("B", [1, 1000])
+def test_small_polygon_box_plan_skips_one_lane_buckets(engine, B):
+    """A plan that cannot fill the GPU never runs a one-lane row-partitioned bucket (one lane
+    through all 11 rows: 84 us per 1,000 pairs against 50 us on the dense rows); the pairs take
+    the dense (6, 1, 12) ball-row kernel in its latency configuration."""
+    b = _solves(_polygon_box(engine, B))
+    assert b and all(not (x["oe"] > 0 and x["lpp"] < 2) for x in b)
+    assert all(x["oe"] == 0 and x["lpp"] >= 4 for x in b)
+
+
+def test_bucket_index_checked(engine):
+    import bench
+    from dcol_amd import DcolLibraryError
+    tab = bench.shape_table(8, 0)
+    ids = _ids(engine, tab)
+    plan = engine.plan(ids[[0, 1]], ids[[2, 3]], cache=False)
+    assert len(plan.buckets()) == plan.num_buckets
+    import ctypes
+    from dcol_amd import _lib
+    info = (ctypes.c_int32 * 8)()
+    n = ctypes.c_int64()
+    with pytest.raises(DcolLibraryError):
+        _lib.check(_lib.load().dcol_plan_bucket(plan.handle, plan.num_buckets, info, ctypes.byref(n)), "dcol_plan_bucket")
