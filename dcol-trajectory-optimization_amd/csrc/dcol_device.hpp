@@ -1042,16 +1042,17 @@ struct Solver {
     // scale), chosen per kernel at compile time (LDL):
     //  * upper Cholesky H = F_c' F_c: F = F_c, idg = 1 / diag(F_c) (v_rsq_f64 + refinement);
     //  * square-root-free H = U' D U (U unit upper, D = diag(d), d_j = F_c[j][j]^2 -- the
-    //    same pivots): F = U, idg = 1 / d (v_rcp_f64 + one Newton step).  The pivots sit on
-    //    the replicated critical path of every PDIP iteration and of initialize(); without the
-    //    square-root refinement the poly x poly loop is 646 -> 614 instructions and its
-    //    Cholesky section 590 -> 476 cycles.  Used by the polytope x polytope kernels (NSOC
-    //    = 0).  The SOC kernels keep the square-root form: the factorisation's extra row
-    //    block (E below) pushed the one-wave N = 6 PART kernels into in-loop scratch (polygon
-    //    x polytope -13 %), and on the 1M mixed workload it moved one polytope x cone pair's
-    //    exit test (mu = tol (1 - 1e-7) in the oracle) across tol -- rounding-decided, but the
-    //    full-size tests hold every pair to the oracle's iteration count.
-    //    -DDCOL_CHOL_SQRT: the square-root form everywhere (A/B runs).
+    //    same pivots): F = U, idg = 1 / d.  The pivots sit on the replicated critical path of
+    //    every PDIP iteration and of initialize(); without the square-root refinement the
+    //    poly x poly loop is 646 -> 614 instructions and its Cholesky section 590 -> 476
+    //    cycles.  Used by every N = 4 kernel (polytope, sphere and cone pairs).  The pivot
+    //    reciprocal is v_rcp_f64 + one Newton step in the polytope x polytope kernels and the
+    //    correctly rounded two-step frcp in the SOC ones: with the one-step reciprocal there,
+    //    one polytope x cone pair of the 1M mixed set (its exit test decided at
+    //    mu = tol (1 - 1e-7) in the oracle) took one more iteration than the oracle.  The
+    //    N = 5 / 6 kernels keep the square-root form: the factorisation's extra row block (E
+    //    below) pushed the one-wave PART kernels into in-loop scratch (polygon x polytope
+    //    -13 %).  -DDCOL_CHOL_SQRT: the square-root form everywhere (A/B runs).
     // False if a pivot is <= 0, infinite or NaN.  Any non-finite entry of H's upper triangle
     // makes some pivot non-finite (a diagonal entry directly, an off-diagonal one through the
     // products that update later pivots), so a non-finite H always fails here and the caller
@@ -1059,7 +1060,7 @@ struct Solver {
 #ifdef DCOL_CHOL_SQRT
     static constexpr bool LDL = false;
 #else
-    static constexpr bool LDL = NSOC == 0;
+    static constexpr bool LDL = N == 4;
 #endif
     DCOL_HD static bool chol(const double (&H)[N][N], double (&F)[N][N], double (&idg)[N]) {
         bool ok = true;
@@ -1070,7 +1071,7 @@ struct Solver {
 #pragma unroll
             for (int k = 0; k < j; ++k) d -= (LDL ? E[LDL ? k : 0][j] : F[k][j]) * F[k][j];
             ok = ok && pos_finite(d);
-            idg[j] = LDL ? frcp1(d) : frsqrt(d);
+            idg[j] = !LDL ? frsqrt(d) : (NSOC == 0 ? frcp1(d) : frcp(d));
 #pragma unroll
             for (int c = j + 1; c < N; ++c) {
                 double t = H[j][c];
