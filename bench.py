@@ -197,6 +197,8 @@ def main():
                     help="mixed1m: all-gather through torch.distributed instead of the C-ABI RCCL path")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process (HIP hardware queues; 0 = leave the environment's)")
+    ap.add_argument("--no-kernel-1m", dest="kernel_1m", action="store_false",
+                    help="skip the 1M-pair kernel-only steady-state section (kernel_1m)")
     ap.add_argument("--pack-pass", action="store_true",
                     help="mixed1m: per-pair arrays + pack_records kernel + out-of-place all-gather instead of "
                          "records written by the solver kernels with the all-gather in place (A/B)")
@@ -292,6 +294,7 @@ def main():
     torch.cuda.synchronize(dev)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     e2e = end_to_end(args, eng, ids, s1, s2, p1, p2, pose1, pose2, out, step, dev) if world == 1 else None
+    k1m = kernel_1m(args, eng, ids, tab, dev) if world == 1 and args.kernel_1m else None
     if dist is not None:
         t = torch.tensor([elapsed, kern_ms, elapsed_serial or 0.0], device=coll_dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -357,6 +360,8 @@ def main():
     }
     if e2e is not None:
         line["end_to_end"] = e2e
+    if k1m is not None:
+        line["kernel_1m"] = k1m
     # spot parity check against the oracle on the first and the last pairs of the timed batch
     # (a graded launch solves its last pairs with the wider lane groups)
     if args.check and args.max_iter == 50:
@@ -389,6 +394,46 @@ def main():
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def kernel_1m(args, eng, ids, tab, dev, reps=20):
+    """The solve kernel's steady state, apart from the 100k launch's quantisation (3,125 waves
+    over 2,048 wave slots: 1.53 rounds, the last one partly empty): ONE launch of 1M pairs of
+    the same distribution (15.3 rounds), kernel only, HIP events on the launch stream (median
+    of `reps` after 5 warm-up launches), with its FP64 roofline fraction (counted flops)."""
+    import torch
+    from dcol_amd import alloc_outputs
+    B = 1_000_000
+    s1, s2, p1, p2 = pairs(B, len(tab["type"]), seed=7)
+    plan = eng.plan(ids[s1], ids[s2], cache=False)
+    d1 = torch.from_numpy(np.ascontiguousarray(p1.T)).to(dev)
+    d2 = torch.from_numpy(np.ascontiguousarray(p2.T)).to(dev)
+    out = alloc_outputs(B, dev, want_grad=True, want_contact=False)
+    stream = torch.cuda.current_stream(dev)
+    run = plan.bind(d1, d2, out, grad=args.grad, contact=False, stream=stream)
+    for _ in range(5):
+        run()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for e0, e1 in ev:
+        e0.record(stream)
+        run()
+        e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
+    st = out["status"].cpu().numpy()
+    it = out["iters"].cpu().numpy()
+    fl = flops_per_pair(it[st == 0], args.grad)
+    tf = fl * B / (ms * 1e-3) / 1e12
+    gbs = BYTES_PER_PAIR * B / (ms * 1e-3) / 1e9
+    del d1, d2, out, plan
+    return {"pairs": B, "kernel_ms": ms, "pair_solves_per_s": B / (ms * 1e-3),
+            "roofline_fp64": {"achieved": tf, "peak": FP64_VECTOR_PEAK_TFS, "unit": "TFLOP/s",
+                              "frac": tf / FP64_VECTOR_PEAK_TFS, "flops_per_pair": fl},
+            "roofline_hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS},
+            "ok_frac": float(np.mean(st == 0)), "iters_mean": float(it[st == 0].mean()),
+            "note": "one 1M-pair launch (same shape table and pose distribution, seed 7), kernel only, median of "
+                    f"{reps} HIP-event launches: the steady-state rate of the solve kernel without the 100k "
+                    "launch's last, partly-filled round of waves"}
 
 
 def end_to_end(args, eng, ids, s1, s2, p1, p2, pose1, pose2, out, step, dev, reps=20):
@@ -570,51 +615,60 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
     gathered = torch.empty((world * cap, REC), dtype=torch.float64, device=dev if comm is not None else coll_dev)
 
     lanes = []
-    if comm is not None:
-        # steps issued round-robin on --streams HIP streams, each with its own communicator
-        # (collectives of one communicator are not issued from two streams) and buffers: the
-        # all-gather of one step overlaps the solve of the next (a batch service's steady
-        # state); the one-stream rate is reported beside it
-        comms = [comm]
-        for _ in range(max(1, args.streams) - 1):
-            c, err = native_comm(NativeComm, dist, world, rank, local)
-            if dist is not None:     # decided together: no rank may go on to another id broadcast alone
-                ok = torch.tensor([0.0 if c is None else 1.0], device=coll_dev)
-                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-                if ok.item() < 1.0 and c is not None:
-                    c.close()
-                    c, err = None, err or "another rank could not create its communicator"
-            if c is None:
-                native_error = f"extra stream communicator: {err}"
-                break
-            comms.append(c)
-        if dist is not None:     # every rank uses the same number of lanes
-            t = torch.tensor([float(len(comms))], device=coll_dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            while len(comms) > int(t.item()):
-                comms.pop().close()
-        for j, c in enumerate(comms):
-            st = stream if j == 0 else torch.cuda.Stream(dev)
-            o = out if j == 0 else alloc_outputs(n, dev, want_grad=True, want_contact=False)
-            r_ = rec if j == 0 else torch.full((cap, REC), float("nan"), dtype=torch.float64, device=dev)
-            g_ = gathered if j == 0 else torch.empty((world * cap, REC), dtype=torch.float64, device=dev)
-            if args.pack_pass:   # the pack kernel + out-of-place all-gather (A/B)
-                lanes.append(lambda c=c, st=st, o=o, r_=r_, g_=g_: c.solve_gather(
-                    plan, d1, d2, cap, grad=args.grad, out=o, stream=st, rec_local=r_, rec_all=g_))
-            else:                # records written by the solver kernels, all-gather in place
-                lanes.append(lambda c=c, st=st, g_=g_: c.solve_gather(
-                    plan, d1, d2, cap, grad=args.grad, stream=st, rec_all=g_, in_place=True, soa=False))
+    if comm is not None and args.pack_pass:
+        # the pack kernel + out-of-place all-gather (A/B): one stream, one communicator
+        def step():
+            comm.solve_gather(plan, d1, d2, cap, grad=args.grad, out=out, stream=stream, rec_local=rec, rec_all=gathered)
 
-        def step():
-            lanes[0]()
+        def solve_only():   # its solve: the plan run with the per-pair arrays
+            launch()
+    elif comm is not None:
+        # records written by the solver kernels, all-gather in place.  Steps are issued
+        # round-robin on --streams solve streams, each with its own gathered buffer; every
+        # all-gather goes through the ONE communicator on ONE collective stream, in issue order
+        # on every rank: step k's solve (DCOL_NO_GATHER) -> event -> its all-gather on the
+        # collective stream -> event that step k + S's solve waits for before it overwrites the
+        # buffer.  So step k + 1's solve overlaps step k's all-gather (a batch service's steady
+        # state) without two communicators or collectives on two streams.
+        cstream = torch.cuda.Stream(dev)
+        nst = max(1, args.streams)
+        bufs = [gathered] + [torch.empty((world * cap, REC), dtype=torch.float64, device=dev) for _ in range(nst - 1)]
+        sstreams = [stream] + [torch.cuda.Stream(dev) for _ in range(nst - 1)]
+        solved = [torch.cuda.Event() for _ in range(nst)]
+        gdone = [torch.cuda.Event() for _ in range(nst)]
+
+        def lane_fn(j):
+            st, g_ = sstreams[j], bufs[j]
+
+            def f():
+                st.wait_event(gdone[j])
+                comm.solve_gather(plan, d1, d2, cap, grad=args.grad, stream=st, rec_all=g_, in_place=True, soa=False,
+                                  gather=False)
+                solved[j].record(st)
+                cstream.wait_event(solved[j])
+                comm.all_gather(cap, g_, stream=cstream)
+                gdone[j].record(cstream)
+            return f
+        lanes = [lane_fn(j) for j in range(nst)]
+
+        def step():          # one step on the launch stream: solve, then the all-gather on it
+            comm.solve_gather(plan, d1, d2, cap, grad=args.grad, stream=stream, rec_all=gathered, in_place=True,
+                              soa=False)
+
+        def solve_only():    # the same solve and record writes without the all-gather (DCOL_NO_GATHER)
+            comm.solve_gather(plan, d1, d2, cap, grad=args.grad, stream=stream, rec_all=gathered, in_place=True,
+                              soa=False, gather=False)
     else:
-        def step():
+        def solve_only():
             launch()
             rec[:n, 0] = out["alpha"]
             rec[:n, 1:13] = out["grad"].T
             # (status, iters) as an int32 pair in the last slot (dcol_amd.dist.REC)
             rec[:n, 13] = ((out["iters"].to(torch.int64) << 32) | (out["status"].to(torch.int64) & 0xFFFFFFFF)).view(
                 torch.float64)
+
+        def step():
+            solve_only()
             if dist is not None:
                 dist.all_gather_into_tensor(gathered, rec.to(coll_dev))
             else:
@@ -642,30 +696,30 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
 
     elapsed_serial = timed([step]) if len(lanes) > 1 else None
     elapsed = timed(lanes if len(lanes) > 1 else [step])
-    # solve-only duration (HIP events on the launch stream; the plan's side-stream buckets
-    # join back into it) -> FP64 roofline with the counted per-class flop model
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
-    for e0, e1 in ev:
-        e0.record(stream)
-        launch()
-        e1.record(stream)
-    torch.cuda.synchronize(dev)
-    solve_ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
-    # the whole step (solve + pack + all-gather) the same way: its excess over the solve is
-    # the communication cost of the step (5-50 % predicted at 8 GPUs)
-    for e0, e1 in ev:
-        e0.record(stream)
-        step()
-        e1.record(stream)
-    torch.cuda.synchronize(dev)
-    step_ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
+
+    def ev_median(fn, reps=10):
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for e0, e1 in ev:
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+        torch.cuda.synchronize(dev)
+        return float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
+    # like for like (HIP events on the launch stream, one step at a time): solve = the step's
+    # own solve and record writes without its collective; step = the same with it; their
+    # difference is the communication cost of the step (5-50 % predicted
+    # at 8 GPUs).  kernel = the plan run with the per-pair arrays (FP64 roofline).
+    solve_ms = ev_median(solve_only)
+    step_ms = ev_median(step)
+    kernel_ms = ev_median(launch)
     my_iters = out["iters"].cpu().numpy()
     my_status = out["status"].cpu().numpy()
     flops_local = mixed_flops(tab, s1[mine], s2[mine], my_iters, my_status, args.grad)
     # per-rank shard figures (load balance): solve ms, step ms, mean Newton iterations
-    mine_stats = [solve_ms, step_ms, float(my_iters[my_status == 0].mean()) if (my_status == 0).any() else 0.0, float(n)]
+    mine_stats = [solve_ms, step_ms, float(my_iters[my_status == 0].mean()) if (my_status == 0).any() else 0.0, float(n),
+                  kernel_ms]
     if dist is not None:
-        t = torch.zeros((world, 4), device=coll_dev, dtype=torch.float64)
+        t = torch.zeros((world, 5), device=coll_dev, dtype=torch.float64)
         t[rank] = torch.tensor(mine_stats, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         ranks_stats = t.cpu().numpy()
@@ -675,8 +729,7 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
     torch.cuda.synchronize(dev)
     allrec = gathered.cpu().numpy().reshape(world, cap, REC)
     if comm is not None:
-        for c in comms:
-            c.close()
+        comm.close()
     if rank != 0:
         return None
     full = np.empty((B, REC))
@@ -697,31 +750,36 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
         "solve_stats": {"ok_frac": float(np.mean(status == 0)), "iters_mean": float(res_all["iters"][status == 0].mean())},
         "solve_ms_rank0": solve_ms, "solve_ms_max_rank": solve_ms_max,
         "step_breakdown": {
-            "note": "HIP events on each rank's launch stream, one step at a time (median of 10): solve = the "
-                    "plan run alone (per-pair arrays); step = the timed step (" + (
-                        "solve + pack_records + all-gather" if args.pack_pass else
-                        "solve writing the records into the gathered buffer + in-place all-gather") +
-                    "); comm = step - solve",
+            "note": "HIP events on each rank's launch stream, one step at a time (median of 10), like for like: "
+                    "solve = the step's own solve and record writes without its collective (" + (
+                        "the plan run with the per-pair arrays; the pack pass + all-gather are the comm"
+                        if args.pack_pass else "dcol_prox_batch_multi_gpu with DCOL_NO_GATHER") +
+                    "); step = the same with the all-gather; comm = step - solve",
             "solve_ms_max_rank": solve_ms_max, "step_ms_max_rank": float(ranks_stats[:, 1].max()),
             "comm_ms_rank0": step_ms - solve_ms, "comm_frac_rank0": (step_ms - solve_ms) / step_ms if step_ms > 0 else None,
             "record_bytes_per_pair": REC * 8,
             "per_rank": {"solve_ms": ranks_stats[:, 0].tolist(), "step_ms": ranks_stats[:, 1].tolist(),
+                         "kernel_ms": ranks_stats[:, 4].tolist(),
                          "iters_mean": ranks_stats[:, 2].tolist(), "pairs": ranks_stats[:, 3].astype(int).tolist()}},
+        "kernel_ms_rank0": kernel_ms,
         "pipeline": {"streams": max(1, len(lanes)), "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                      "serial_value": B * steps / elapsed_serial if elapsed_serial else B * steps / elapsed,
                      "serial_ms_per_step": 1e3 * (elapsed_serial or elapsed) / steps},
     }
     if comm is not None:
         line["rccl_world_size"] = world
+        line["collective_issue"] = ("one communicator, all-gathers in issue order on one collective stream, "
+                                    "chained to the solve streams by events" if not args.pack_pass else
+                                    "one communicator, one stream")
     if native_error:
         line["native_comm_error"] = native_error
     if flops_local is not None:
-        tf = flops_local / (solve_ms * 1e-3) / 1e12
+        tf = flops_local / (kernel_ms * 1e-3) / 1e12
         line["roofline_fp64"] = {"bound": "fp64-valu", "achieved": tf, "peak": FP64_VECTOR_PEAK_TFS,
                                  "unit": "TFLOP/s", "frac": tf / FP64_VECTOR_PEAK_TFS,
                                  "flops_per_pair": flops_local / max(n, 1),
                                  "note": "rank 0's shard: counted per-class flops (profiles/flop_model.json) at each "
-                                         "pair's iteration count / the shard's solve time (HIP events)"}
+                                         "pair's iteration count / the shard's plan-run time (kernel_ms_rank0, HIP events)"}
     if args.check:
         from oracle import c_oracle
         k = min(args.check * 8, B)

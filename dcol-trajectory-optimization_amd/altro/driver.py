@@ -30,6 +30,7 @@ against whole-run fixtures of the reference itself).
 from __future__ import annotations
 
 import dataclasses
+import inspect
 import logging
 import os
 import time
@@ -80,6 +81,14 @@ class _Timed:
     def __init__(self, field):
         self.field = field
         self.async_ = hasattr(field, "submit") and hasattr(field, "collect")
+        # evaluators written against the two-value contract (evaluate(poses, grad) ->
+        # (alpha, J), raising on a failed pair) have no raise_ keyword: collect(raise_=False)
+        # then calls them the old way and reports an all-zero status
+        fn = field.collect if self.async_ else field.evaluate
+        try:
+            self.has_raise = "raise_" in inspect.signature(fn).parameters
+        except (TypeError, ValueError):
+            self.has_raise = False
         self.seconds = 0.0
         self.batches = 0
         self.pairs = 0
@@ -102,11 +111,13 @@ class _Timed:
         t0 = time.perf_counter()
         poses, grad = self._job
         self._job = None
-        kw = {} if raise_ else {"raise_": False}
+        kw = {} if (raise_ or not self.has_raise) else {"raise_": False}
         if self.soa:
             out = self.field.collect(soa=True, **kw)
         else:
             out = self.field.collect(**kw) if self.async_ else self.field.evaluate(poses, grad, **kw)
+        if not raise_ and not kw:       # a two-value evaluator: it raised on a failed pair already
+            out = (out[0], out[1], np.zeros(np.shape(out[0]), dtype=np.int32))
         self.seconds += time.perf_counter() - t0
         self.batches += 1
         self.pairs += poses.shape[0] * out[0].shape[1]
@@ -154,10 +165,16 @@ def solve(params, X, U, prox=None, engine=None, verbose=True, prox_wide=None) ->
 
     params/X/U: as returned by altro.systems.<system>.initialize() (or the reference's own
     initialize_<system>()).  prox: constraint evaluator with
-    ``evaluate(victim_poses [N, 6], grad) -> (alpha [N, n_obs], J [N, n_obs, 12] | None)``;
-    default: an ObstacleField on the GPU (constraints.py).  prox_wide: the same evaluator
-    over TRIALS * N knots (line-search retries, TRIALS trajectories per batch); default: an
-    ObstacleField when prox is None, else retries go through prox one at a time.
+    ``evaluate(victim_poses [N, 6], grad) -> (alpha [N, n_obs], J [N, n_obs, 12] | None)``
+    that raises (like the reference) on a failed pair; default: an ObstacleField on the GPU
+    (constraints.py).  prox_wide: the same evaluator over TRIALS * N knots (line-search
+    retries, TRIALS trajectories per batch); default: an ObstacleField when prox is None,
+    else retries go through prox one at a time.  The retries are read with
+    ``evaluate(..., raise_=False)`` (or ``collect(raise_=False)``) ->
+    ``(alpha, J, status [N, n_obs] int32)`` when the evaluator takes that keyword, so that a
+    failed pair raises only if its trial is the one the reference would evaluate; an
+    evaluator without it is called the two-value way (it raises on any failed pair of the
+    batch, and its status is taken as all zero).
     params['reg'] / ['rho'] /
     ['X_hist'] / ['U_hist'] are updated in place like the reference does."""
     t_setup = time.perf_counter()

@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <list>
 #include <map>
 #include <mutex>
 #include <string>
@@ -124,9 +125,12 @@ struct dcol_table {
     // of the device (device_side_streams), shared by every table
     hipStream_t side[kSideStreams] = {};
     bool side_ready = false;
-    // dcol_prox_pair: one-pair plans per (shape1, shape2), a stream, and device-mapped pinned
-    // staging [pose1 (6) | pose2 (6) | alpha | contact (3) | grad (12) | (iters, status)]
-    std::unordered_map<int64_t, dcol_plan*> pair_plans;
+    // dcol_prox_pair: one-pair plans per (shape1, shape2), at most DCOL_PAIR_PLANS_MAX, least
+    // recently used first out (pair_lru: most recent at the front), a stream, and
+    // device-mapped pinned staging [pose1 (6) | pose2 (6) | alpha | contact (3) | grad (12) |
+    // (iters, status)]
+    std::list<std::pair<int64_t, dcol_plan*>> pair_lru;
+    std::unordered_map<int64_t, std::list<std::pair<int64_t, dcol_plan*>>::iterator> pair_plans;
     hipStream_t pair_stream = nullptr;
     double* pair_host = nullptr;
     double* pair_dev = nullptr;
@@ -266,7 +270,7 @@ int dcol_table_create(const dcol_shape_desc* shapes, int32_t n, int32_t device, 
 int dcol_table_destroy(dcol_table* t) {
     if (!t) return DCOL_SUCCESS;
     DeviceGuard g(t->device);
-    for (auto& kv : t->pair_plans) dcol_plan_destroy(kv.second);
+    for (auto& kv : t->pair_lru) dcol_plan_destroy(kv.second);
     if (t->pair_stream) (void)hipStreamDestroy(t->pair_stream);
     if (t->pair_host) (void)hipHostFree(t->pair_host);
     if (t->d_shapes) (void)hipFree(t->d_shapes);
@@ -383,6 +387,11 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
         const int ball = c.nsoc == 0 ? 0
                          : (none_cone && !ball_disabled()) ? 1
                          : (all_cone && c.N == 4 && !cone_disabled()) ? 2 : 0;
+        // a row-partitioned bucket only where its SOC flavour is compiled: the x polytope
+        // (NSOC = 1) buckets exist only with ball rows, so with DCOL_NO_BALL those pairs take
+        // the dense-row kernels (N and NSOC do not depend on the partition, so `ball` stands)
+        if (c.status == DCOL_OK && c.oe > 0 && !part_flavour_built(c.N, c.nsoc, c.omax, c.oe, c.lpp, ball == 1))
+            c = classify(a, b, case4, false);
         // flavour's own list (row-partitioned buckets have theirs: PairClass::lpp)
         if (c.status == DCOL_OK && ball && c.oe == 0) c.lpp = choose_lpp(c.N, c.nsoc, c.omax, 2 * ball);
         Key k = c.status == DCOL_OK ? Key{0, c.N, c.nsoc, c.omax, c.lpp, ball, 0, c.oe} : Key{1, 0, 0, 0, 0, 0, c.status, 0};
@@ -602,10 +611,20 @@ int bucket_and_fuse(const dcol_table* t, int64_t B, const int32_t* s1, const int
         rc = bucket_pairs(t, B, s1, s2, p, perm, case4, false, true);
         if (rc != DCOL_SUCCESS) return rc;
     }
-    if (plan_fuse(t, p, true) == 2) {
+    // only when every bucket the fused kernel lacks is a row-partitioned one (a dense bucket
+    // without a case -- a many-row bucket -- keeps the plan unfused whatever the PART pairs
+    // do, and they would lose their faster kernels for nothing); when the re-bucketed plan
+    // still does not fuse, the first bucketing stands
+    bool only_part = true;
+    for (const Launch& L : p->launches)
+        if (L.kind == 0 && L.oe == 0 && fused_vid(L.N, L.nsoc, L.omax, L.lpp, L.flags(), 0) < 0) only_part = false;
+    if (plan_fuse(t, p, true) == 2 && only_part) {
         rc = bucket_pairs(t, B, s1, s2, p, perm, case4, true, lat_part);
         if (rc != DCOL_SUCCESS) return rc;
-        plan_fuse(t, p, true);
+        if (plan_fuse(t, p, true) == 2) {
+            rc = bucket_pairs(t, B, s1, s2, p, perm, case4, false, lat_part);
+            if (rc != DCOL_SUCCESS) return rc;
+        }
     }
     if (!allow_fuse && p->fused()) {   // same buckets, launched one by one (fan-out)
         p->segs.clear();
@@ -864,12 +883,23 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
     const int64_t key = (int64_t)s1 * ns + s2;
     const bool c4 = (flags & DCOL_CASE4) != 0;
     const int64_t ck = c4 ? -1 - key : key;   // case-4 plans apart
+    dcol_plan* plan = nullptr;
     auto it = t->pair_plans.find(ck);
-    if (it == t->pair_plans.end()) {
-        dcol_plan* p = nullptr;
-        const int rc = dcol_plan_create_ex(t, 1, &s1, &s2, c4 ? DCOL_PLAN_CASE4 : 0, &p);
+    if (it != t->pair_plans.end()) {
+        t->pair_lru.splice(t->pair_lru.begin(), t->pair_lru, it->second);   // now the most recent
+        plan = it->second->second;
+    } else {
+        const int rc = dcol_plan_create_ex(t, 1, &s1, &s2, c4 ? DCOL_PLAN_CASE4 : 0, &plan);
         if (rc != DCOL_SUCCESS) return rc;
-        it = t->pair_plans.emplace(ck, p).first;
+        // the least recently used plan makes room (no launch of it is in flight: every call
+        // synchronises its stream before returning)
+        if ((int)t->pair_lru.size() >= DCOL_PAIR_PLANS_MAX) {
+            t->pair_plans.erase(t->pair_lru.back().first);
+            dcol_plan_destroy(t->pair_lru.back().second);
+            t->pair_lru.pop_back();
+        }
+        t->pair_lru.emplace_front(ck, plan);
+        t->pair_plans.emplace(ck, t->pair_lru.begin());
     }
     double* h = t->pair_host;
     double* d = t->pair_dev;
@@ -878,7 +908,7 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
     int32_t* hi = reinterpret_cast<int32_t*>(h + 28);
     int32_t* di = reinterpret_cast<int32_t*>(d + 28);
     // SoA of one pair = the 6 values in order; the kernel reads / writes the mapped memory
-    int rc = dcol_plan_run(it->second, d, d + 6, tol, max_iter, flags & ~DCOL_CASE4, d + 12, d + 13, d + 16, di, di + 1,
+    int rc = dcol_plan_run(plan, d, d + 6, tol, max_iter, flags & ~DCOL_CASE4, d + 12, d + 13, d + 16, di, di + 1,
                            t->pair_stream);
     if (rc != DCOL_SUCCESS) return rc;
     const hipError_t e = hipStreamSynchronize(t->pair_stream);
@@ -888,6 +918,14 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
     if (grad && (flags & DCOL_GRAD_ANY)) std::memcpy(grad, h + 16, 12 * sizeof(double));
     if (iters) *iters = hi[0];
     if (status) *status = hi[1];
+    return DCOL_SUCCESS;
+}
+
+int dcol_table_pair_plans(const dcol_table* tc, int32_t* n) {
+    if (!tc || !n) return fail(DCOL_ERR_ARG, "dcol_table_pair_plans: NULL argument");
+    dcol_table* t = const_cast<dcol_table*>(tc);
+    std::lock_guard<std::mutex> lk(t->mu);
+    *n = (int32_t)t->pair_lru.size();
     return DCOL_SUCCESS;
 }
 
@@ -1040,30 +1078,43 @@ struct Rccl {
     bool ok = false;
 };
 
+// The collective library: librccl, or the one DCOL_RCCL_LIB names (a test stand-in with
+// the same five entry points, tests/fake_rccl/), resolved per library path on first use
 const Rccl& rccl() {
-    static Rccl r = [] {
-        Rccl x;
-        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    static std::mutex mu;
+    static std::map<std::string, Rccl> libs;
+    const char* env = std::getenv("DCOL_RCCL_LIB");
+    const std::string path = (env && *env) ? env : "";
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = libs.find(path);
+    if (it != libs.end()) return it->second;
+    Rccl x;
+    void* h = nullptr;
+    if (!path.empty()) {
+        h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+    } else {
+        h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
         if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
-        if (!h) return x;
+    }
+    if (h) {
         x.get_unique_id = reinterpret_cast<decltype(&ncclGetUniqueId)>(dlsym(h, "ncclGetUniqueId"));
         x.init_rank = reinterpret_cast<decltype(&ncclCommInitRank)>(dlsym(h, "ncclCommInitRank"));
         x.destroy = reinterpret_cast<decltype(&ncclCommDestroy)>(dlsym(h, "ncclCommDestroy"));
         x.all_gather = reinterpret_cast<decltype(&ncclAllGather)>(dlsym(h, "ncclAllGather"));
         x.error_string = reinterpret_cast<decltype(&ncclGetErrorString)>(dlsym(h, "ncclGetErrorString"));
         x.ok = x.get_unique_id && x.init_rank && x.destroy && x.all_gather && x.error_string;
-        return x;
-    }();
-    return r;
+    }
+    return libs.emplace(path, x).first->second;   // std::map: references stay valid
 }
 
-std::string rccl_error(ncclResult_t r) {
-    return rccl().error_string ? rccl().error_string(r) : std::to_string((int)r);
+std::string rccl_error(const Rccl& api, ncclResult_t r) {
+    return api.error_string ? api.error_string(r) : std::to_string((int)r);
 }
 
 }  // namespace
 
 struct dcol_comm {
+    const Rccl* api = nullptr;   // the library the communicator was made with
     ncclComm_t comm = nullptr;
     int32_t nranks = 0, rank = 0, device = 0;
 };
@@ -1106,10 +1157,11 @@ extern "C" {
 
 int dcol_comm_unique_id(uint8_t id[DCOL_COMM_ID_BYTES]) {
     if (!id) return fail(DCOL_ERR_ARG, "dcol_comm_unique_id: id is NULL");
-    if (!rccl().ok) return fail(DCOL_ERR_HIP, "dcol_comm_unique_id: librccl not loadable");
+    const Rccl& api = rccl();
+    if (!api.ok) return fail(DCOL_ERR_HIP, "dcol_comm_unique_id: librccl not loadable");
     ncclUniqueId u;
-    ncclResult_t r = rccl().get_unique_id(&u);
-    if (r != ncclSuccess) return fail(DCOL_ERR_HIP, "ncclGetUniqueId: " + rccl_error(r));
+    ncclResult_t r = api.get_unique_id(&u);
+    if (r != ncclSuccess) return fail(DCOL_ERR_HIP, "ncclGetUniqueId: " + rccl_error(api, r));
     static_assert(sizeof(u.internal) == DCOL_COMM_ID_BYTES, "unique id size");
     std::memcpy(id, u.internal, DCOL_COMM_ID_BYTES);
     return DCOL_SUCCESS;
@@ -1120,16 +1172,18 @@ int dcol_comm_create(const uint8_t id[DCOL_COMM_ID_BYTES], int32_t nranks, int32
     if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks || device < 0)
         return fail(DCOL_ERR_ARG, "dcol_comm_create: bad arguments");
     *out = nullptr;
-    if (!rccl().ok) return fail(DCOL_ERR_HIP, "dcol_comm_create: librccl not loadable");
+    const Rccl& api = rccl();
+    if (!api.ok) return fail(DCOL_ERR_HIP, "dcol_comm_create: librccl not loadable");
     DeviceGuard g(device);
     ncclUniqueId u;
     std::memcpy(u.internal, id, DCOL_COMM_ID_BYTES);
     auto* c = new (std::nothrow) dcol_comm();
     if (!c) return fail(DCOL_ERR_NOMEM, "dcol_comm_create");
-    ncclResult_t r = rccl().init_rank(&c->comm, nranks, u, rank);
+    c->api = &api;
+    ncclResult_t r = api.init_rank(&c->comm, nranks, u, rank);
     if (r != ncclSuccess) {
         delete c;
-        return fail(DCOL_ERR_HIP, "ncclCommInitRank: " + rccl_error(r));
+        return fail(DCOL_ERR_HIP, "ncclCommInitRank: " + rccl_error(api, r));
     }
     c->nranks = nranks;
     c->rank = rank;
@@ -1140,7 +1194,7 @@ int dcol_comm_create(const uint8_t id[DCOL_COMM_ID_BYTES], int32_t nranks, int32
 
 int dcol_comm_destroy(dcol_comm* c) {
     if (!c) return DCOL_SUCCESS;
-    if (c->comm) (void)rccl().destroy(c->comm);
+    if (c->comm) (void)c->api->destroy(c->comm);
     delete c;
     return DCOL_SUCCESS;
 }
@@ -1153,7 +1207,9 @@ int dcol_prox_batch_multi_gpu(const dcol_plan* p, dcol_comm* c, const double* po
     if (cap < p->B) return fail(DCOL_ERR_ARG, "dcol_prox_batch_multi_gpu: cap < shard size");
     if (p->table->device != c->device)
         return fail(DCOL_ERR_ARG, "dcol_prox_batch_multi_gpu: plan and communicator on different devices");
-    const int32_t rflags = flags & ~DCOL_CONTACT;   // the record carries no contact point
+    const bool gather = (flags & DCOL_NO_GATHER) == 0;
+    if (!gather && rec_local) return fail(DCOL_ERR_ARG, "dcol_prox_batch_multi_gpu: DCOL_NO_GATHER is in place only");
+    const int32_t rflags = flags & ~(DCOL_CONTACT | DCOL_NO_GATHER);   // the record carries no contact point
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (!rec_local) {
         // in place: the solver epilogues write this rank's records straight into its slice of
@@ -1169,8 +1225,9 @@ int dcol_prox_batch_multi_gpu(const dcol_plan* p, dcol_comm* c, const double* po
                                                 (size_t)(cap - p->B) * DCOL_REC * sizeof(double), st);
             if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("record tail: ") + hipGetErrorString(e));
         }
-        ncclResult_t r = rccl().all_gather(mine, rec_all, (size_t)cap * DCOL_REC, ncclDouble, c->comm, st);
-        if (r != ncclSuccess) return fail(DCOL_ERR_HIP, "ncclAllGather: " + rccl_error(r));
+        if (!gather) return DCOL_SUCCESS;
+        ncclResult_t r = c->api->all_gather(mine, rec_all, (size_t)cap * DCOL_REC, ncclDouble, c->comm, st);
+        if (r != ncclSuccess) return fail(DCOL_ERR_HIP, "ncclAllGather: " + rccl_error(*c->api, r));
         return DCOL_SUCCESS;
     }
     int rc = dcol_plan_run(p, pose1, pose2, tol, max_iter, rflags, alpha, nullptr,
@@ -1185,8 +1242,18 @@ int dcol_prox_batch_multi_gpu(const dcol_plan* p, dcol_comm* c, const double* po
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("pack_records: ") + hipGetErrorString(e));
     }
-    ncclResult_t r = rccl().all_gather(rec_local, rec_all, (size_t)cap * DCOL_REC, ncclDouble, c->comm, st);
-    if (r != ncclSuccess) return fail(DCOL_ERR_HIP, "ncclAllGather: " + rccl_error(r));
+    ncclResult_t r = c->api->all_gather(rec_local, rec_all, (size_t)cap * DCOL_REC, ncclDouble, c->comm, st);
+    if (r != ncclSuccess) return fail(DCOL_ERR_HIP, "ncclAllGather: " + rccl_error(*c->api, r));
+    return DCOL_SUCCESS;
+}
+
+int dcol_comm_all_gather(dcol_comm* c, int64_t cap, double* rec_all, void* stream) {
+    if (!c || !rec_all || cap < 0) return fail(DCOL_ERR_ARG, "dcol_comm_all_gather: bad arguments");
+    DeviceGuard g(c->device);
+    double* mine = rec_all + (size_t)c->rank * (size_t)cap * DCOL_REC;
+    ncclResult_t r = c->api->all_gather(mine, rec_all, (size_t)cap * DCOL_REC, ncclDouble, c->comm,
+                                        reinterpret_cast<hipStream_t>(stream));
+    if (r != ncclSuccess) return fail(DCOL_ERR_HIP, "ncclAllGather: " + rccl_error(*c->api, r));
     return DCOL_SUCCESS;
 }
 

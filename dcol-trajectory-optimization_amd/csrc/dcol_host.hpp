@@ -199,6 +199,17 @@ inline int part_lpp(int N, int nsoc, int omax, int oe, bool latency = false) {
     return first;
 }
 
+// A PART kernel of the bucket at lpp whose SOC flavour a launch may use: ball rows (FL bit 1)
+// only when every SOC block of the pair is a ball block (ball), else the dense SOC rows
+inline bool part_flavour_built(int N, int nsoc, int omax, int oe, int lpp, bool ball) {
+    bool built = false;
+#define DCOL_PFB(NN, NS, OM, LP, WP, FL, OEE) \
+    if (NN == N && NS == nsoc && OM == omax && OEE == oe && LP == lpp && (ball || (FL & 2) == 0)) built = true;
+    DCOL_PART_VARIANTS(DCOL_PFB)
+#undef DCOL_PFB
+    return built;
+}
+
 // Row-partitioned bucket of a pair with op pose rows and oe extra-column rows (N = 5 / 6,
 // one primitive with extra columns): the smallest (omax, oe) holding both, fewest slots
 // first, then fewest extra slots (DCOL_PART_SHAPES is sorted that way per (N, NSOC));

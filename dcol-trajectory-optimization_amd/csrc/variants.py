@@ -162,11 +162,25 @@ PART = {
     # measured 200k pairs: capsule x box 8.1e8 at LPP 2 -> 9.5e8, cylinder x box 6.6 -> 7.1e8)
     (5, 1): {(8, 2): [(1, 1), (2, 1)], (10, 2): [(1, 1), (2, 1)], (14, 2): [(2, 1)], (18, 2): [(2, 1)]},
     # x sphere / cone: both lanes own a SOC block (capsule x sphere 11.2e8 at LPP 2, 9.1e8 at 1)
-    (5, 2): {(2, 2): [(2, 1), (1, 1)], (4, 2): [(2, 1), (1, 1)], (6, 2): [(2, 1)]},
+    # two waves per SIMD where the allocator then spills at most a few scratch accesses per
+    # iteration (tools/isa_stats.py --waves 2) -- measured 200k pairs per class
+    # (profiles/r04_wps/): capsule x cone 7.82e8 -> 8.68e8, cone x capsule 7.92 -> 8.94e8
+    # ((4, 2), 2 scratch accesses per iteration), cylinder x cone 6.88 -> 7.35e8, cone x
+    # cylinder 6.78 -> 7.35e8 ((6, 2), 21)
+    (5, 2): {(2, 2): [(2, 1), (1, 1)], (4, 2): [(2, 2), (1, 1)], (6, 2): [(2, 2)]},
     (6, 1): {(9, 3): [(1, 1)], (10, 4): [(1, 1), (2, 1)], (11, 5): [(1, 1)], (12, 6): [(1, 1), (2, 1)],
              (14, 8): [(2, 1)]},
     # pentagon x sphere 7.6e8 at LPP 2 (6, 6) against 6.9e8 at LPP 1 (5, 5)
     (6, 2): {(4, 4): [(2, 1)], (6, 4): [(2, 1)], (6, 6): [(2, 1), (1, 1)], (8, 6): [(2, 1)], (8, 8): [(2, 1)]},
+}
+# per-flavour overrides of PART: (N, NSOC, OMAX, OE, "ball" | "dense") -> [(LPP, WPS), ...].  The
+# ball-row copies of the polygon x sphere buckets hold fewer registers than the dense ones and
+# run two waves per SIMD (4 / 0 scratch accesses per iteration): pentagon x sphere 7.88e8 ->
+# 8.99e8, sphere x pentagon 8.01 -> 9.07e8 ((6, 6)); the dense copies spill far more there
+# (polygon x cone in (8, 6) at two waves: 5.98e8 -> 2.77e8), so they keep one wave.
+PART_FL = {
+    (6, 2, 4, 4, "ball"): [(2, 2)],
+    (6, 2, 6, 6, "ball"): [(2, 2), (1, 1)],
 }
 
 
@@ -176,9 +190,14 @@ def part_flavours(n, nsoc):
     return [3, 2] + ([1, 0] if nsoc == 2 else [])
 
 
+def part_configs(n, s, o, oe, fl):
+    """(LPP, WPS) list of one PART bucket's copies of flavour fl (first = throughput choice)"""
+    return PART_FL.get((n, s, o, oe, "ball" if fl & 2 else "dense"), PART[(n, s)][(o, oe)])
+
+
 def part_variants():
-    return [(n, s, o, l, w, fl, oe) for (n, s), bl in sorted(PART.items()) for (o, oe), cf in sorted(bl.items())
-            for fl in part_flavours(n, s) for l, w in cf]
+    return [(n, s, o, l, w, fl, oe) for (n, s), bl in sorted(PART.items()) for (o, oe) in sorted(bl)
+            for fl in part_flavours(n, s) for l, w in part_configs(n, s, o, oe, fl)]
 
 
 # (N, NSOC, OMAX, LPP, WPS, FL without the SUSP bit, OE): the benchmark's poly x poly kernel
@@ -196,9 +215,8 @@ def fused_part():
         for (o, oe), cf in sorted(bl.items()):
             if s != 2 or o > FUSE_PART_OMAX:
                 continue
-            lpp = max(l for l, _ in cf)
             for fl in (3, 2):
-                out.append((n, s, o, lpp, fl, oe))
+                out.append((n, s, o, max(l for l, _ in part_configs(n, s, o, oe, fl)), fl, oe))
     return out
 
 

@@ -17,12 +17,13 @@ POLYTOPE, SPHERE, CONE, CAPSULE, CYLINDER, POLYGON = range(6)
 # enum dcol_status
 OK, MAXITER, UNSUPPORTED, NOT_PD, NONFINITE, TOO_LARGE = range(6)
 # enum dcol_flags
-GRAD_FD, GRAD_ENVELOPE, CONTACT, CASE4, GRAD_IMPLICIT = 1, 2, 4, 8, 16
+GRAD_FD, GRAD_ENVELOPE, CONTACT, CASE4, GRAD_IMPLICIT, NO_GATHER = 1, 2, 4, 8, 16, 32
 GRAD_ANY = GRAD_FD | GRAD_ENVELOPE | GRAD_IMPLICIT
 # enum dcol_plan_options
 PLAN_CASE4, PLAN_NO_FUSE, PLAN_SUSPEND = 1, 2, 4
 SUCCESS, ERR_ARG, ERR_HIP, ERR_NOMEM = 0, -1, -2, -3
-ABI_VERSION = 2
+ABI_VERSION = 3
+PAIR_PLANS_MAX = 64   # DCOL_PAIR_PLANS_MAX
 
 
 class DcolLibraryError(RuntimeError):
@@ -60,12 +61,14 @@ SIGNATURES = {
                                      c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "dcol_prox_pair": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_double, c_int32, c_int32, c_void_p,
                                c_void_p, c_void_p, c_void_p, c_void_p]),
+    "dcol_table_pair_plans": (c_int, [c_void_p, POINTER(c_int32)]),
     "dcol_comm_unique_id": (c_int, [c_void_p]),
     "dcol_comm_create": (c_int, [c_void_p, c_int32, c_int32, c_int32, POINTER(c_void_p)]),
     "dcol_comm_destroy": (c_int, [c_void_p]),
     "dcol_prox_batch_multi_gpu": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_double, c_int32, c_int32,
                                           c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                           c_void_p]),
+    "dcol_comm_all_gather": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
 }
 COMM_ID_BYTES = 128
 

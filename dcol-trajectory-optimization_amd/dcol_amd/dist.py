@@ -134,7 +134,7 @@ class NativeComm:
         return bytes(buf)
 
     def solve_gather(self, plan, pose1, pose2, cap: int, tol=1e-6, max_iter=50, grad="fd", out=None,
-                     stream=None, rec_local=None, rec_all=None, in_place=False, soa=True):
+                     stream=None, rec_local=None, rec_all=None, in_place=False, soa=True, gather=True):
         """Solve this rank's shard (``plan`` over its pairs; torch float64 [6, n] poses on the
         device) and all-gather the packed records: returns (out, rec_all) with rec_all a
         torch float64 [world * cap, REC] tensor (rank r's shard at rows r * cap), asynchronous
@@ -143,7 +143,9 @@ class NativeComm:
         in_place: the kernels write the records straight into this rank's rows of rec_all and
         the all-gather runs in place (include/dcol.h, rec_local == NULL); rows past the shard
         are all-ones bytes (NaN, int pair (-1, -1)).  soa=False (in place only): no per-pair
-        output arrays, records only (out is returned as None)."""
+        output arrays, records only (out is returned as None).  gather=False (in place only,
+        DCOL_NO_GATHER): everything but the all-gather -- issue it with :meth:`all_gather`
+        (e.g. on a stream of its own), or time the step without its collective."""
         import ctypes
 
         import torch
@@ -154,6 +156,8 @@ class NativeComm:
             raise ValueError("in_place writes into rec_all: pass no rec_local")
         if not soa and not in_place:
             raise ValueError("soa=False needs in_place=True (the pack pass reads the per-pair arrays)")
+        if not gather and not in_place:
+            raise ValueError("gather=False needs in_place=True")
         n = plan.B
         dev = torch.device("cuda", self.device)
         for t in (pose1, pose2):
@@ -161,7 +165,7 @@ class NativeComm:
                 raise ValueError(f"poses must be contiguous float64 [6, {n}] on {dev}")
         if cap < n:
             raise ValueError("cap must be >= the shard size")
-        flags = grad_flag(grad)
+        flags = grad_flag(grad) | (0 if gather else _lib.NO_GATHER)
         if stream is None:
             stream = torch.cuda.current_stream(dev)
         # Buffers allocated here belong to `stream` in torch's caching allocator (allocated
@@ -171,7 +175,7 @@ class NativeComm:
         # also be passed in (hot loops reuse them; then the caller owns their lifetime).
         with torch.cuda.stream(stream):
             if out is None and soa:
-                out = alloc_outputs(n, dev, bool(flags), False)
+                out = alloc_outputs(n, dev, bool(flags & _lib.GRAD_ANY), False)
             if rec_local is None and not in_place:
                 rec_local = torch.empty((cap, REC), dtype=torch.float64, device=dev)
             if rec_all is None:
@@ -187,6 +191,28 @@ class NativeComm:
             ptr(o.get("alpha")), ptr(o.get("grad")), ptr(o.get("iters")), ptr(o.get("status")), ptr(rec_local),
             ptr(rec_all), ctypes.c_void_p(stream.cuda_stream)), "dcol_prox_batch_multi_gpu")
         return (out if soa else None), rec_all
+
+    def all_gather(self, cap: int, rec_all, stream=None):
+        """The in-place all-gather alone (dcol_comm_all_gather): every rank's rows
+        [rank * cap, (rank + 1) * cap) of rec_all (torch float64 [world * cap, REC] on this
+        rank's device) to every rank, asynchronous on ``stream``.  Follows a
+        ``solve_gather(..., in_place=True, gather=False)`` whose stream the caller orders
+        before ``stream`` (an event)."""
+        import ctypes
+
+        import torch
+
+        from . import _lib
+        dev = torch.device("cuda", self.device)
+        shape = (self.world * int(cap), REC)
+        if (rec_all.dtype != torch.float64 or tuple(rec_all.shape) != shape or not rec_all.is_contiguous()
+                or rec_all.device != dev):
+            raise ValueError(f"rec_all must be contiguous float64 {shape} on {dev}")
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        _lib.check(_lib.load().dcol_comm_all_gather(self.handle, int(cap), ctypes.c_void_p(rec_all.data_ptr()),
+                                                    ctypes.c_void_p(stream.cuda_stream)), "dcol_comm_all_gather")
+        return rec_all
 
     def close(self):
         from . import _lib

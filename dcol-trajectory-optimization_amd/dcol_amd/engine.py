@@ -341,26 +341,29 @@ class Engine:
         """One pair at its current poses -> (alpha, contact [3] | None, grad [12] | None,
         iters, status): the drop-in's per-call path (dcol_prox_pair: a cached one-pair plan
         and device-mapped pinned staging, one kernel launch, no copy commands).  The returned
-        arrays are fresh copies."""
-        s1 = self.register_object(prim1)
-        s2 = self.register_object(prim2)
-        table = self.table
-        st = self._pair
-        if st is None:
-            bufs = (np.empty(12), np.empty(1), np.empty(3), np.empty(12), np.empty(2, dtype=np.int32))
-            st = self._pair = (bufs, [ctypes.c_void_p(b.ctypes.data) for b in bufs], _lib.load().dcol_prox_pair)
-        (pose, alpha, cp, g, ints), (a_pose, a_alpha, a_cp, a_g, a_ints), fn = st
-        pose[0:3] = np.reshape(prim1.r, 3)     # read at every call, like the reference (pose_of)
-        pose[3:6] = np.reshape(prim1.p, 3)
-        pose[6:9] = np.reshape(prim2.r, 3)
-        pose[9:12] = np.reshape(prim2.p, 3)
+        arrays are fresh copies.  Thread-safe: the engine's one staging set is held under the
+        engine lock from the pose writes to the output copies (two threads on the default
+        engine would otherwise overwrite each other's poses or outputs)."""
         flags = grad_flag(grad) | (_lib.CONTACT if contact else 0)
-        rc = fn(table.handle, s1, s2, a_pose, ctypes.c_void_p(a_pose.value + 48), tol, self.max_iter, flags,
-                a_alpha, a_cp, a_g, a_ints, ctypes.c_void_p(a_ints.value + 4))
-        if rc:
-            _lib.check(rc, "dcol_prox_pair")
-        return (alpha[0], cp.copy() if contact else None, g.copy() if flags & _lib.GRAD_ANY else None,
-                int(ints[0]), int(ints[1]))
+        with self._lock:
+            s1 = self.register_object(prim1)
+            s2 = self.register_object(prim2)
+            table = self.table
+            st = self._pair
+            if st is None:
+                bufs = (np.empty(12), np.empty(1), np.empty(3), np.empty(12), np.empty(2, dtype=np.int32))
+                st = self._pair = (bufs, [ctypes.c_void_p(b.ctypes.data) for b in bufs], _lib.load().dcol_prox_pair)
+            (pose, alpha, cp, g, ints), (a_pose, a_alpha, a_cp, a_g, a_ints), fn = st
+            pose[0:3] = np.reshape(prim1.r, 3)     # read at every call, like the reference (pose_of)
+            pose[3:6] = np.reshape(prim1.p, 3)
+            pose[6:9] = np.reshape(prim2.r, 3)
+            pose[9:12] = np.reshape(prim2.p, 3)
+            rc = fn(table.handle, s1, s2, a_pose, ctypes.c_void_p(a_pose.value + 48), tol, self.max_iter, flags,
+                    a_alpha, a_cp, a_g, a_ints, ctypes.c_void_p(a_ints.value + 4))
+            if rc:
+                _lib.check(rc, "dcol_prox_pair")
+            return (np.float64(alpha[0]), cp.copy() if contact else None, g.copy() if flags & _lib.GRAD_ANY else None,
+                    int(ints[0]), int(ints[1]))
 
 
 _default: Engine | None = None

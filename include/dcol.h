@@ -37,7 +37,8 @@
 extern "C" {
 #endif
 
-#define DCOL_ABI_VERSION 2   /* 2: 14-slot multi-GPU record (status / iters as an int32 pair) */
+#define DCOL_ABI_VERSION 3   /* 2: 14-slot multi-GPU record (status / iters as an int32 pair);
+                                3: DCOL_NO_GATHER + dcol_comm_all_gather, dcol_table_pair_plans */
 
 /* Primitive types (misc_primitive_constructor.py:4-88). */
 enum dcol_shape_type {
@@ -68,12 +69,18 @@ enum dcol_flags {
     DCOL_CONTACT = 4,       /* write x[0:3] (proximity.py:51-54)                          */
     DCOL_CASE4 = 8,         /* dcol_prox_batch_host only: solve case-4 pairs (see
                                DCOL_PLAN_CASE4) instead of reporting DCOL_UNSUPPORTED     */
-    DCOL_GRAD_IMPLICIT = 16 /* implicit-function derivative of the returned iterate: the
+    DCOL_GRAD_IMPLICIT = 16, /* implicit-function derivative of the returned iterate: the
                                KKT system linearised with the NT scaling at (x, s, z),
                                d alpha = e3' H^-1 (-dG'z - G'W^-2 (dG x - dh)) with H the
                                PDIP's normal matrix G'W^-2 G (same Cholesky routine), for
                                the 12 pose coordinates; equals the envelope gradient as
                                mu -> 0 (pdip.py:434; no reference counterpart)            */
+    DCOL_NO_GATHER = 32     /* dcol_prox_batch_multi_gpu in place only: the solve and the
+                               record writes of the call (this rank's rows of rec_all and
+                               their NaN tail) WITHOUT the all-gather -- issue it with
+                               dcol_comm_all_gather (e.g. on a stream of its own, so the
+                               next step's solve overlaps it), or time the step without
+                               its collective (comm = step - this, like for like)         */
 };
 #define DCOL_GRAD_ANY (DCOL_GRAD_FD | DCOL_GRAD_ENVELOPE | DCOL_GRAD_IMPLICIT)
 
@@ -190,13 +197,20 @@ int dcol_prox_batch_host(const dcol_table* table, int64_t B, const int32_t* shap
 int dcol_prox_pair(const dcol_table* table, int32_t shape1, int32_t shape2, const double* pose1,
                    const double* pose2, double tol, int32_t max_iter, int32_t flags, double* alpha,
                    double* contact, double* grad, int32_t* iters, int32_t* status);
+/* One-pair plans dcol_prox_pair holds (least recently used evicted past DCOL_PAIR_PLANS_MAX,
+ * so device memory stays bounded however many distinct shape pairs a caller queries).  */
+#define DCOL_PAIR_PLANS_MAX 64
+int dcol_table_pair_plans(const dcol_table* table, int32_t* n);
 
 /* ---- multi-GPU ------------------------------------------------------
  * One process per GPU.  Pairs are independent, so each rank solves its own shard with its
  * own plan; when one consumer needs the whole batch, dcol_prox_batch_multi_gpu packs the
  * shard's results and performs ONE all-gather (RCCL over xGMI, librccl loaded on first
  * use).  Bootstrap: rank 0 calls dcol_comm_unique_id and ships the 128 bytes to the other
- * ranks by the host's own means (the reference's Python: torch.distributed / a file).  */
+ * ranks by the host's own means (the reference's Python: torch.distributed / a file).
+ * The collective library is librccl unless the environment names another one in
+ * DCOL_RCCL_LIB when the id / the communicator is made (tests: an in-process stand-in that
+ * runs several ranks as threads on one GPU, tests/fake_rccl/).                           */
 #define DCOL_COMM_ID_BYTES 128
 /* packed per-pair record, 14 x 8 B = 112 B: alpha, grad[12] (float64), then status and iters
  * as two int32 (little-endian: status in the low half) in the last 8-byte slot           */
@@ -217,11 +231,17 @@ int dcol_comm_destroy(dcol_comm* comm);
  * rank's rows of rec_all (rows n..cap-1: all-ones bytes, i.e. NaN doubles and the int pair
  * (-1, -1)) and the all-gather runs in place (sendbuff = rec_all + rank * cap * DCOL_REC):
  * no pack pass and no local copy.  alpha / grad / iters / status are then optional (NULL:
- * records only; given: filled as well).                                                  */
+ * records only; given: filled as well).  flags | DCOL_NO_GATHER (in place only): everything
+ * but the all-gather.                                                                    */
 int dcol_prox_batch_multi_gpu(const dcol_plan* plan, dcol_comm* comm, const double* pose1, const double* pose2,
                               double tol, int32_t max_iter, int32_t flags, int64_t cap, double* alpha,
                               double* grad, int32_t* iters, int32_t* status, double* rec_local,
                               double* rec_all, void* stream);
+/* The in-place all-gather alone: every rank's rows [rank * cap, (rank + 1) * cap) of
+ * rec_all[nranks * cap][DCOL_REC] to every rank, asynchronous on `stream` (after a
+ * DCOL_NO_GATHER solve; the caller orders the two streams, e.g. with an event).  Issue the
+ * collectives of one communicator in the same order on every rank.                      */
+int dcol_comm_all_gather(dcol_comm* comm, int64_t cap, double* rec_all, void* stream);
 
 #ifdef __cplusplus
 }

@@ -263,6 +263,25 @@ def test_wide_line_search_ignores_failures_of_unevaluated_trials():
               prox_wide=_poisoned_wide(params, N, g["alpha"], True), verbose=False)
 
 
+def test_wide_two_value_evaluator_contract():
+    """a prox_wide evaluator written against the two-value contract
+    (evaluate(poses, grad) -> (alpha, J), no raise_ keyword) still drives the batched
+    retries -- called the old way, status taken as all zero -- with the reference's decisions."""
+    from altro import solve, systems
+    from altro.driver import TRIALS
+    from altro_cpu import OracleField
+
+    class TwoValue(OracleField):
+        def evaluate(self, poses, grad):
+            return super().evaluate(poses, grad)
+    g = np.load(os.path.join(GOLDEN, "altro", "altro_quadrotor.npz"))
+    params, X, U = systems.initialize("quadrotor")
+    N = params["N"]
+    r = solve(params, X, U, prox=OracleField(params["P_vic"], params["P_obs"], N),
+              prox_wide=TwoValue(params["P_vic"], params["P_obs"], TRIALS * N), verbose=False)
+    check_run(r, g)
+
+
 def test_reg_max_raises_like_reference():
     """update_reg (ALTRO.py:51-74): a failed line search at reg == reg_max is a ValueError."""
     from altro import solve, systems

@@ -53,3 +53,20 @@ def test_package_layout():
     for sub in ("proximity/proximity.py", "proximity/proximity_gradient.py", "primitives/misc_primitive_constructor.py",
                 "dcol_amd/_lib.py", "csrc/dcol_device.hpp", "csrc/dcol_capi.cpp"):
         assert os.path.exists(os.path.join(PKG, sub)), sub
+
+
+def test_header_constants_match_binding():
+    """flag / size constants of include/dcol.h that dcol_amd._lib restates"""
+    from dcol_amd import _lib
+    txt = open(HEADER).read()
+
+    def val(name):
+        m = re.search(rf"\b{name}\s*=\s*(\d+)", txt) or re.search(rf"#define\s+{name}\s+(\d+)", txt)
+        assert m, name
+        return int(m.group(1))
+    assert val("DCOL_NO_GATHER") == _lib.NO_GATHER
+    assert val("DCOL_GRAD_IMPLICIT") == _lib.GRAD_IMPLICIT
+    assert val("DCOL_CASE4") == _lib.CASE4
+    assert val("DCOL_PAIR_PLANS_MAX") == _lib.PAIR_PLANS_MAX
+    assert val("DCOL_ABI_VERSION") == _lib.ABI_VERSION
+    assert val("DCOL_REC") == 14

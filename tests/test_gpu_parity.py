@@ -275,3 +275,91 @@ def test_native_comm_side_stream(engine):
         u = unpack(rec.cpu().numpy())
         np.testing.assert_array_equal(u["alpha"], ref["alpha"].cpu().numpy())
         np.testing.assert_array_equal(u["grad"], ref["grad"].cpu().numpy().T)
+
+
+def test_pair_plan_cache_bounded(engine):
+    """dcol_prox_pair keeps at most DCOL_PAIR_PLANS_MAX one-pair plans (least recently used
+    out): 100 distinct shape pairs through it, each result at the parity tolerances against
+    the reference's golden values with equal iteration counts, the cache never above the cap,
+    and a pair whose plan was evicted solves bitwise as on its first call."""
+    import ctypes
+
+    from dcol_amd import _lib
+    d = load_golden([p for p in golden_files() if p.endswith("synthetic_mixed.npz")][0])
+    s1, s2 = register(engine, d)
+    lib = _lib.load()
+    table = engine.table
+    sel = np.flatnonzero(d["status"] == 0)[:100]
+    assert len(set(zip(s1[sel].tolist(), s2[sel].tolist()))) == 100 > _lib.PAIR_PLANS_MAX
+
+    def call(i):
+        p1 = np.ascontiguousarray(d["pose1"][i], dtype=np.float64)
+        p2 = np.ascontiguousarray(d["pose2"][i], dtype=np.float64)
+        a, c, g = np.empty(1), np.empty(3), np.empty(12)
+        it, st = ctypes.c_int32(), ctypes.c_int32()
+        ptr = lambda x: ctypes.c_void_p(x.ctypes.data)  # noqa: E731
+        _lib.check(lib.dcol_prox_pair(table.handle, int(s1[i]), int(s2[i]), ptr(p1), ptr(p2), 1e-6, 50,
+                                      _lib.GRAD_FD | _lib.CONTACT, ptr(a), ptr(c), ptr(g), ctypes.byref(it),
+                                      ctypes.byref(st)), "dcol_prox_pair")
+        return a[0], g.copy(), int(it.value), int(st.value)
+
+    n = ctypes.c_int32()
+    first = {}
+    for i in sel:
+        a, g, it, st = call(i)
+        first[i] = (a, g)
+        assert st == 0 and it == d["iters"][i]
+        assert alpha_close(a, d["alpha"][i]) and grad_close(g, d["grad"][i])
+        _lib.check(lib.dcol_table_pair_plans(table.handle, ctypes.byref(n)), "dcol_table_pair_plans")
+        assert n.value <= _lib.PAIR_PLANS_MAX
+    assert n.value == _lib.PAIR_PLANS_MAX
+    a, g, _, _ = call(sel[0])          # evicted long ago: a fresh plan, the same bits
+    assert a == first[sel[0]][0] and np.array_equal(g, first[sel[0]][1])
+
+
+_NO_BALL_SCRIPT = r"""
+import sys, numpy as np
+sys.path[:0] = [sys.argv[2], sys.argv[3]]
+from dcol_amd import Engine, spec_from_arrays
+d = dict(np.load(sys.argv[4], allow_pickle=False))
+K = 100                                   # 150k pairs: a plan that fills the GPU (throughput buckets)
+eng = Engine(device=0)
+ids = np.array([eng.register(spec_from_arrays(d, k)) for k in range(len(d["type"]))], np.int32)
+s1, s2 = np.tile(ids[d["s1"]], K), np.tile(ids[d["s2"]], K)
+r = eng.solve_host(s1, s2, np.tile(d["pose1"], (K, 1)), np.tile(d["pose2"], (K, 1)), grad="fd", contact=False)
+b = eng.plan(s1, s2).buckets()
+np.savez(sys.argv[1], alpha=r.alpha, grad=r.grad, iters=r.iters, status=r.status,
+         part=np.array([x["oe"] for x in b]), flags=np.array([x["flags"] for x in b]))
+"""
+
+
+@pytest.mark.parametrize("var", ["DCOL_NO_BALL", "DCOL_NO_CONE", "DCOL_NO_PART"])
+def test_mixed_golden_large_plan_env_variants(tmp_path, var):
+    """The documented A/B switches on a plan large enough for the throughput buckets (the
+    mixed golden set tiled to 150k pairs): DCOL_NO_BALL (no ball-row kernels: the x polytope
+    row-partitioned buckets, compiled with ball rows only, must fall back to the dense rows
+    instead of failing the launch), DCOL_NO_CONE, DCOL_NO_PART -- status and iteration counts
+    equal to the reference's on every pair, alpha and gradient at the parity tolerances."""
+    import os
+    import subprocess
+    import sys
+
+    from conftest import PKG, REPO
+    path = [p for p in golden_files() if p.endswith("synthetic_mixed.npz")][0]
+    env = {k: v for k, v in os.environ.items() if k not in ("DCOL_NO_BALL", "DCOL_NO_CONE", "DCOL_NO_PART", "DCOL_LPP")}
+    env[var] = "1"
+    f = str(tmp_path / "out.npz")
+    subprocess.run([sys.executable, "-c", _NO_BALL_SCRIPT, f, PKG, REPO, path], check=True, env=env, timeout=240)
+    r = dict(np.load(f))
+    d = load_golden(path)
+    K = len(r["alpha"]) // len(d["alpha"])
+    st, it = np.tile(d["status"], K), np.tile(d["iters"], K)
+    np.testing.assert_array_equal(r["status"], st)
+    ok = st == 0
+    np.testing.assert_array_equal(r["iters"][ok], it[ok])
+    assert np.all(alpha_close(r["alpha"][ok], np.tile(d["alpha"], K)[ok]))
+    assert np.all(grad_close(r["grad"][ok], np.tile(d["grad"], (K, 1))[ok]))
+    if var == "DCOL_NO_BALL":
+        assert not np.any((r["flags"] & 2) != 0)
+    if var == "DCOL_NO_PART":
+        assert not np.any(r["part"] > 0)
