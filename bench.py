@@ -697,21 +697,23 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
     elapsed_serial = timed([step]) if len(lanes) > 1 else None
     elapsed = timed(lanes if len(lanes) > 1 else [step])
 
-    def ev_median(fn, reps=10):
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-        for e0, e1 in ev:
-            e0.record(stream)
-            fn()
-            e1.record(stream)
+    def ev_medians(fns, reps=20):
+        """median HIP-event duration of each fn, the fns interleaved rep by rep (the same clock
+        state for all of them)"""
+        ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in fns]
+              for _ in range(reps)]
+        for row in ev:
+            for fn, (e0, e1) in zip(fns, row):
+                e0.record(stream)
+                fn()
+                e1.record(stream)
         torch.cuda.synchronize(dev)
-        return float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
-    # like for like (HIP events on the launch stream, one step at a time): solve = the step's
-    # own solve and record writes without its collective; step = the same with it; their
-    # difference is the communication cost of the step (5-50 % predicted
-    # at 8 GPUs).  kernel = the plan run with the per-pair arrays (FP64 roofline).
-    solve_ms = ev_median(solve_only)
-    step_ms = ev_median(step)
-    kernel_ms = ev_median(launch)
+        return [float(np.median([row[i][0].elapsed_time(row[i][1]) for row in ev])) for i in range(len(fns))]
+    # like for like (HIP events on the launch stream, one step at a time, interleaved): solve =
+    # the step's own solve and record writes without its collective; step = the same with it;
+    # their difference is the communication cost of the step (SURVEY.md section 8e: 5-50 %
+    # predicted at 8 GPUs).  kernel = the plan run with the per-pair arrays (FP64 roofline).
+    solve_ms, step_ms, kernel_ms = ev_medians([solve_only, step, launch])
     my_iters = out["iters"].cpu().numpy()
     my_status = out["status"].cpu().numpy()
     flops_local = mixed_flops(tab, s1[mine], s2[mine], my_iters, my_status, args.grad)
@@ -750,7 +752,8 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
         "solve_stats": {"ok_frac": float(np.mean(status == 0)), "iters_mean": float(res_all["iters"][status == 0].mean())},
         "solve_ms_rank0": solve_ms, "solve_ms_max_rank": solve_ms_max,
         "step_breakdown": {
-            "note": "HIP events on each rank's launch stream, one step at a time (median of 10), like for like: "
+            "note": "HIP events on each rank's launch stream, one step at a time (median of 20, the three "
+                    "measurements interleaved), like for like: "
                     "solve = the step's own solve and record writes without its collective (" + (
                         "the plan run with the per-pair arrays; the pack pass + all-gather are the comm"
                         if args.pack_pass else "dcol_prox_batch_multi_gpu with DCOL_NO_GATHER") +

@@ -134,6 +134,7 @@ struct dcol_table {
     hipStream_t pair_stream = nullptr;
     double* pair_host = nullptr;
     double* pair_dev = nullptr;
+    int32_t pair_seq = 0;   // completion flag value of the last one-pair launch
 };
 
 struct Launch {
@@ -760,9 +761,10 @@ int dcol_plan_bucket(const dcol_plan* p, int32_t i, int32_t info[8], int64_t* pa
 namespace {
 // dcol_plan_run with an optional record output (rec: [B][DCOL_REC], written by the solver
 // epilogues; then alpha / grad / iters / status may be NULL)
+// done / done_seq: completion flag of a one-pair plan (dcol_prox_pair; KArgs::done)
 int plan_run_rec(const dcol_plan* p, const double* pose1, const double* pose2, double tol, int32_t max_iter,
                  int32_t flags, double* alpha, double* contact, double* grad, int32_t* iters, int32_t* status,
-                 double* rec, void* stream) {
+                 double* rec, void* stream, int32_t* done = nullptr, int32_t done_seq = 0) {
     if (!p) return fail(DCOL_ERR_ARG, "dcol_plan_run: NULL plan");
     if (p->B == 0) return DCOL_SUCCESS;
     if (!pose1 || !pose2 || (!alpha && !rec))
@@ -797,6 +799,8 @@ int plan_run_rec(const dcol_plan* p, const double* pose1, const double* pose2, d
     a.susp_pi = nullptr;
     a.susp_state = nullptr;
     a.susp_cap = 0;
+    a.done = done;
+    a.done_seq = done_seq;
     const bool fan = p->lanes > 1 && p->fork;
     hipError_t e = hipSuccess;
     if (fan) {
@@ -867,10 +871,11 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
     dcol_table* t = const_cast<dcol_table*>(tc);
     std::lock_guard<std::mutex> lk(t->mu);
     DeviceGuard g(t->device);
-    constexpr int kSlots = 12 + 1 + 3 + 12 + 1;
+    constexpr int kSlots = 12 + 1 + 3 + 12 + 1 + 1;   // ... | (iters, status) | completion flag
     if (!t->pair_host) {
         hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&t->pair_host), kSlots * sizeof(double),
                                      hipHostMallocMapped | hipHostMallocPortable);
+        if (e == hipSuccess) std::memset(t->pair_host, 0, kSlots * sizeof(double));   // the flag word starts at 0
         if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&t->pair_dev), t->pair_host, 0);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&t->pair_stream, hipStreamNonBlocking);
         if (e != hipSuccess) {
@@ -907,12 +912,41 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
     std::memcpy(h + 6, pose2, 6 * sizeof(double));
     int32_t* hi = reinterpret_cast<int32_t*>(h + 28);
     int32_t* di = reinterpret_cast<int32_t*>(d + 28);
-    // SoA of one pair = the 6 values in order; the kernel reads / writes the mapped memory
-    int rc = dcol_plan_run(plan, d, d + 6, tol, max_iter, flags & ~DCOL_CASE4, d + 12, d + 13, d + 16, di, di + 1,
-                           t->pair_stream);
+    // SoA of one pair = the 6 values in order; the kernel reads / writes the mapped memory.
+    // Completion: a one-launch solve plan releases a sequence number into the mapped flag
+    // word after its output stores (KArgs::done), and this thread polls host memory for it
+    // -- no stream synchronisation on the latency path; the stream is queried now and then,
+    // so a launch that ends without the flag (or fails) is still caught.  Other plans (a
+    // rejected pair) synchronise the stream.
+    volatile int32_t* hflag = reinterpret_cast<volatile int32_t*>(h + 29);
+    int32_t* dflag = reinterpret_cast<int32_t*>(d + 29);
+    const bool flagged = plan->launches.size() == 1 && plan->launches[0].kind == 0 && !plan->fused() &&
+                         !plan->launches[0].susp && plan->lanes <= 1;
+    const int32_t seq = flagged ? (t->pair_seq = t->pair_seq % 0x7ffffffe + 1) : 0;   // 1 .. 2^31 - 2, never 0
+    int rc = plan_run_rec(plan, d, d + 6, tol, max_iter, flags & ~DCOL_CASE4, d + 12, d + 13, d + 16, di, di + 1,
+                          nullptr, t->pair_stream, flagged ? dflag : nullptr, seq);
     if (rc != DCOL_SUCCESS) return rc;
-    const hipError_t e = hipStreamSynchronize(t->pair_stream);
-    if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_prox_pair: ") + hipGetErrorString(e));
+    if (flagged) {
+        bool seen = false;
+        for (uint64_t spin = 1;; ++spin) {
+            if (__atomic_load_n(const_cast<int32_t*>(hflag), __ATOMIC_ACQUIRE) == seq) {
+                seen = true;
+                break;
+            }
+            if ((spin & 4095) == 0) {
+                const hipError_t q = hipStreamQuery(t->pair_stream);
+                if (q == hipSuccess) {
+                    seen = __atomic_load_n(const_cast<int32_t*>(hflag), __ATOMIC_ACQUIRE) == seq;
+                    break;
+                }
+                if (q != hipErrorNotReady) return fail(DCOL_ERR_HIP, std::string("dcol_prox_pair: ") + hipGetErrorString(q));
+            }
+        }
+        if (!seen) return fail(DCOL_ERR_HIP, "dcol_prox_pair: the launch ended without its completion flag");
+    } else {
+        const hipError_t e = hipStreamSynchronize(t->pair_stream);
+        if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_prox_pair: ") + hipGetErrorString(e));
+    }
     *alpha = h[12];
     if (contact && (flags & DCOL_CONTACT)) std::memcpy(contact, h + 13, 3 * sizeof(double));
     if (grad && (flags & DCOL_GRAD_ANY)) std::memcpy(grad, h + 16, 12 * sizeof(double));

@@ -181,6 +181,12 @@ struct KArgs {
     int32_t* susp_pi;                   // [susp_cap] pair index (slot index into perm space)
     double* susp_state;                 // [fields][susp_cap]: it, x[N], then (s, z, r) per lane row
     int64_t susp_cap;
+    // One-pair launches of dcol_prox_pair (a single workgroup): after every output store of
+    // the launch, thread 0 stores done_seq to *done -- device-mapped pinned host memory,
+    // system-scope release -- so the caller polls host memory for completion instead of
+    // synchronising the stream.  nullptr: none.
+    int32_t* done = nullptr;
+    int32_t done_seq = 0;
 #ifdef DCOL_STAMPS
     unsigned long long* stamps;         // diagnostic build only (tools/stamp_probe.hip): [B][16]
 #endif
@@ -723,7 +729,7 @@ struct Solver {
     DCOL_HD void assemble(const KArgs& A, const DevShape& S1, const DevShape& S2, const Frame& F1, const Frame& F2) {
         o1 = S1.n_ort;
         o = o1 + S2.n_ort;
-        xo2 = (S1.n_extra > 0 && S2.n_extra > 0) ? S1.n_extra : 0;
+        xo2 = (N >= 6 && S1.n_extra > 0 && S2.n_extra > 0) ? S1.n_extra : 0;
         deg = o + NSOC;                                   // quirk Q7
         const double* __restrict__ rows = reinterpret_cast<const double*>(A.rows);
         if constexpr (PART) {
@@ -1125,12 +1131,14 @@ struct Solver {
         for (int j = 0; j < N; ++j) v[j] = R::sum(v[j]);
     }
 
-    // bring2cone, pdip.py:237-287 (quirk Q11), group-wide
+    // bring2cone, pdip.py:237-287 (quirk Q11), group-wide.  FULL: every orthant slot holds a
+    // row (the padding masks fold away, as in the PDIP loop)
+    template <bool FULL>
     DCOL_HD void bring2cone(double* v) const {
         double any = 0.0, mn = __builtin_inf(), socv = -__builtin_inf();
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
-            const bool vk = vort(k);
+            const bool vk = live<FULL>(k);
             any = (vk & (v[k] <= 0.0)) ? 1.0 : any;
             mn = vk ? fmin(mn, v[k]) : mn;
         }
@@ -1149,13 +1157,14 @@ struct Solver {
         if (a >= 0.0) {
             const double sh = 1.0 + a;
 #pragma unroll
-            for (int k = 0; k < OR; ++k) v[k] = vort(k) ? v[k] + sh : v[k];
+            for (int k = 0; k < OR; ++k) v[k] = live<FULL>(k) ? v[k] + sh : v[k];
 #pragma unroll
             for (int b = 0; b < SS; ++b) v[OR + SD * b] = vs[b] ? v[OR + SD * b] + sh : v[OR + SD * b];
         }
     }
 
     // -------- initialize, pdip.py:291-332 ------------------------------------------------
+    template <bool FULL>
     DCOL_HD bool initialize() {
         DCOL_NSTAMP(0);
         double H[N][N], F[N][N], idg[N], gth[N];
@@ -1226,7 +1235,7 @@ struct Solver {
             t[k] = r[k];
         }
         DCOL_NSTAMP(3);
-        bring2cone(t);
+        bring2cone<FULL>(t);
         DCOL_NSTAMP(4);
         // quirk Q1: y = solve_triangular(L, -c) with lower=False reads diag(L) only:
         // y = -e_3 / L_33, then x = L^-T y
@@ -1236,11 +1245,11 @@ struct Solver {
 #pragma unroll
         for (int k = 0; k < M; ++k) zt[k] = rowdot(k, xz);
         DCOL_NSTAMP(5);
-        bring2cone(zt);
+        bring2cone<FULL>(zt);
         DCOL_NSTAMP(6);
 #pragma unroll
         for (int k = 0; k < M; ++k) {
-            const bool v = vrow(k);
+            const bool v = k < OR ? live<FULL>(k) : vrow(k);
             const double one = (k < OR || ((k - OR) % SD) == 0) ? 1.0 : 0.0;   // inert: e
             s[k] = v ? t[k] : one;
             z[k] = v ? zt[k] : one;
@@ -1682,7 +1691,7 @@ struct Solver {
         LagAgg g;
         g.u[0] = g.u[1] = g.u[2] = 0.0;
         g.zs[0] = g.zs[1] = g.zs[2] = g.zs[3] = 0.0;
-        g.kind = S.soc_kind;
+        g.kind = NSOC > 0 ? S.soc_kind : SOC_NONE;   // polytope pairs: no record read
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
             if (PART && k >= PL) continue;   // extra-column rows: G[k][0:3] = 0
@@ -1720,14 +1729,69 @@ struct Solver {
 #pragma unroll
         for (int c = 0; c < 3; ++c) w[c] = Fr.Qe[c] * g.u[0] + Fr.Qe[3 + c] * g.u[1] + Fr.Qe[6 + c] * g.u[2];
     }
-    DCOL_HD double lag_pose_part(const LagAgg& g, const double* v, const DevShape& S, int prim, const Frame& Fr) const {
-        double d[3];
+    // y'Q(p) b for the reference's DCM (problem_matrices.py:213-251) without forming it:
+    // Q(p) = I + (8 (p p' - S I) + al K) / den with S = p'p, al = 4 S - 4, den = (1 + S)^2 and
+    // K b = b x p (dcm_jacobian's Nm), so
+    //   y'Q b = y.b + (8 (y.p)(p.b) - 8 S (y.b) + al p.(y x b)) / den.
+    // The p-independent y.b is left out (returned: the p-dependent correction only) -- it
+    // cancels in a forward difference, and leaving it out keeps its rounding out of the
+    // difference.  yb = y.b and c = y x b are the caller's (p-independent).
+    DCOL_HD static double qcorr(const double* y, const double* b, double yb, const double* c, const double* p,
+                                double S, double al, double iden) {
+        const double yp = y[0] * p[0] + y[1] * p[1] + y[2] * p[2];
+        const double pb = p[0] * b[0] + p[1] * b[1] + p[2] * b[2];
+        const double pc = p[0] * c[0] + p[1] * c[1] + p[2] * c[2];
+        const double t = fma(-S, yb, yp * pb);
+        return fma(al, pc, 8.0 * t) * iden;
+    }
+    DCOL_HD static void cross3(const double* a, const double* b, double* c) {
+        c[0] = a[1] * b[2] - a[2] * b[1];
+        c[1] = a[2] * b[0] - a[0] * b[2];
+        c[2] = a[0] * b[1] - a[1] * b[0];
+    }
+
+    // scipy approx_fprime(theta, f, sqrt(eps)) restricted to primitive prim's 6 coordinates
+    // (proximity_gradient.py:50-88) for f_k(theta) = z'(G(theta) x - h(theta)) over the rows
+    // of primitive k, on its aggregate ag (lag_aggregate: u = sum of z_i G_i[0:3] in the world
+    // frame, the SOC duals zs; group sums already taken).  Every row is linear in the frame
+    // (Qe, r_eff) (see LagAgg), so with Q = Q(p), Qe = Q Q_off, r_eff = r + Q r_off:
+    //   f(r, p) = (Q w').(x - r) - w'.r_off + zs.r + zs.(Q y) + const,
+    //   w' = Q(p0)' u (= Q_off w, w = Qe(p0)' u the body-frame aggregate; Q_off a rotation),
+    //   y = r_off + Q_off (xe0, xe1, 0) (xe: the primitive's extra columns of x),
+    // zs the ball SOC duals 1..3 (zero for other primitives).
+    //  * translations: f is affine in r, so its forward difference is (zs - u)_j whatever the
+    //    step (exact in exact arithmetic; taken in closed form).
+    //  * rotations: forward differences with the reference's step rule of f in closed form
+    //    (qcorr: no DCM is formed), the quotient through the reciprocal of the exact step.
+    // Rounding-level against re-assembling the rows at each perturbed pose (the reference),
+    // which the parity tests bound (1e-5 of max(|g|, 0.01) against the reference's own FD).
+    DCOL_HD void fd_grad_prim(const LagAgg& ag, const DevShape& S, int prim, const double th0[6], double* g) const {
+        const double hstep = 1.4901161193847656e-08;   // sqrt(finfo(float).eps)
+        double zs[3] = {0.0, 0.0, 0.0};
+        if (ag.kind == SOC_BALL) {
+            zs[0] = ag.zs[1]; zs[1] = ag.zs[2]; zs[2] = ag.zs[3];
+        }
 #pragma unroll
-        for (int c = 0; c < 3; ++c) d[c] = x[c] - Fr.re[c];
-        double f = 0.0;
+        for (int j = 0; j < 3; ++j) g[j] = zs[j] - ag.u[j];
+        const double* p0 = th0 + 3;
+        // w' = Q(p0)' u = Q(-p0) u:  u + (8 p (p.u) - 8 S u - al (u x p)) / den
+        const double S0 = p0[0] * p0[0] + p0[1] * p0[1] + p0[2] * p0[2];
+        const double s10 = 1.0 + S0;
+        const double iden0 = frcp(s10 * s10);
+        const double al0 = 4.0 * S0 - 4.0;
+        double wq[3], up[3];
+        cross3(ag.u, p0, up);
+        const double pu = p0[0] * ag.u[0] + p0[1] * ag.u[1] + p0[2] * ag.u[2];
 #pragma unroll
-        for (int r = 0; r < 3; ++r) f += (Fr.Qe[3 * r] * v[0] + Fr.Qe[3 * r + 1] * v[1] + Fr.Qe[3 * r + 2] * v[2]) * d[r];
-        if (g.kind == SOC_BALL) {
+        for (int k = 0; k < 3; ++k) wq[k] = fma(fma(8.0 * p0[k], pu, -8.0 * S0 * ag.u[k]) - al0 * up[k], iden0, ag.u[k]);
+        double d[3], cd[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) d[k] = x[k] - th0[k];
+        cross3(d, wq, cd);
+        const double dw = d[0] * wq[0] + d[1] * wq[1] + d[2] * wq[2];
+        // ball primitives: zs.(Q y)
+        double y[3] = {0.0, 0.0, 0.0}, cz[3] = {0.0, 0.0, 0.0}, zy = 0.0;
+        if constexpr (NSOC > 0) {
             const int off = xoff(prim == 1);
             double xe0 = 0.0, xe1 = 0.0;
 #pragma unroll
@@ -1736,47 +1800,31 @@ struct Solver {
                 if (S.n_extra >= 2 && j == 5 + off) xe1 = x[j];
             }
 #pragma unroll
-            for (int k = 0; k < 3; ++k) f += g.zs[k + 1] * (Fr.re[k] + Fr.Qe[3 * k] * xe0 + Fr.Qe[3 * k + 1] * xe1);
+            for (int k = 0; k < 3; ++k) y[k] = S.r_off[k] + S.Q_off[3 * k] * xe0 + S.Q_off[3 * k + 1] * xe1;
+            cross3(zs, y, cz);
+            zy = zs[0] * y[0] + zs[1] * y[1] + zs[2] * y[2];
         }
-        return f;
-    }
-
-    // scipy approx_fprime(theta, f, sqrt(eps)) restricted to primitive prim's 6 coordinates
-    // (proximity_gradient.py:50-88): forward differences of f_k with the reference's step
-    // rule, f_k evaluated through lag_pose_part on the aggregate ag (lag_aggregate, group
-    // sums already taken).  Translation perturbations keep the rotation (only r_eff moves).
-    // The quotient uses the reciprocal of the exact step dx_j (rounding-level).
-    DCOL_HD void fd_grad_prim(const LagAgg& ag, const DevShape& S, int prim, const double th0[6], double* g) const {
-        const double hstep = 1.4901161193847656e-08;   // sqrt(finfo(float).eps)
-        double tj[6], idx[6];
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            double hj = hstep;
-            if ((th0[j] + hstep) - th0[j] == 0.0)       // _numdiff: fall back to a relative step
-                hj = hstep * (th0[j] >= 0.0 ? 1.0 : -1.0) * fmax(1.0, fabs(th0[j]));
-            tj[j] = th0[j] + hj;
-            idx[j] = frcp(tj[j] - th0[j]);
-        }
-        Frame F0;
-        make_frame(S, th0, F0);
-        double w[3];
-        body_w(ag, F0, w);
-        const double f0 = lag_pose_part(ag, w, S, prim, F0);
+        // f(p) - (p-independent terms), at p0 and at the three perturbed rotations
+        auto fr = [&](const double* p) {
+            const double Sp = p[0] * p[0] + p[1] * p[1] + p[2] * p[2];
+            const double s1 = 1.0 + Sp;
+            const double iden = frcp(s1 * s1);
+            const double al = 4.0 * Sp - 4.0;
+            double f = qcorr(d, wq, dw, cd, p, Sp, al, iden);
+            if constexpr (NSOC > 0) f += qcorr(zs, y, zy, cz, p, Sp, al, iden);
+            return f;
+        };
+        const double f0 = fr(p0);
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            Frame Fj = F0;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) Fj.re[c] = (c == j ? tj[j] : th0[c]) + F0.qro[c];
-            g[j] = (lag_pose_part(ag, w, S, prim, Fj) - f0) * idx[j];
-        }
-#pragma unroll
-        for (int j = 3; j < 6; ++j) {
-            double th[6];
-#pragma unroll
-            for (int c = 0; c < 6; ++c) th[c] = (c == j) ? tj[j] : th0[c];
-            Frame Fj;
-            make_frame(S, th, Fj);
-            g[j] = (lag_pose_part(ag, w, S, prim, Fj) - f0) * idx[j];
+            const double t0 = p0[j];
+            double hj = hstep;
+            if ((t0 + hstep) - t0 == 0.0)       // _numdiff: fall back to a relative step
+                hj = hstep * (t0 >= 0.0 ? 1.0 : -1.0) * fmax(1.0, fabs(t0));
+            const double tj = t0 + hj;
+            double p[3] = {p0[0], p0[1], p0[2]};
+            p[j] = tj;
+            g[3 + j] = (fr(p) - f0) * frcp(tj - t0);
         }
     }
 
@@ -1966,7 +2014,8 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1) {
     make_frame(S2, th2, F2, plain2);
     DCOL_STAMP(A, pi, q, 1);
 
-    Solver<N, NSOC, OMAX, LPP, BALL, CONE, OE> P;
+    using Slv = Solver<N, NSOC, OMAX, LPP, BALL, CONE, OE>;
+    Slv P;
     P.q = q;
 #ifdef DCOL_STAMPS
     P.dbg = (q == 0) ? A.stamps + 16 * pi + 8 : nullptr;
@@ -1979,7 +2028,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1) {
         const int it0 = P.load_state(A, ci);
         st = P.template pdip<FULL>(A.tol, A.max_iter, &it, it0);
     } else {
-        const bool init_ok = P.initialize();
+        const bool init_ok = P.template initialize<FULL>();
         DCOL_STAMP(A, pi, q, 3);
         if (!init_ok) st = ST_NOT_PD;
         else st = P.template pdip<FULL, MODE == 1>(A.tol, A.max_iter, &it, 0, A.susp_t, A.susp_min);
@@ -2015,7 +2064,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1) {
             // lane differentiates one primitive: lane q takes primitive q & 1, so a 2+-lane
             // group does the two 6-coordinate gradients side by side instead of both in
             // every lane (a 1-lane group does both in turn)
-            using Agg = typename Solver<N, NSOC, OMAX, LPP, BALL, CONE, OE>::LagAgg;
+            using Agg = typename Slv::LagAgg;
             const Agg ag0 = P.lag_aggregate(T1, 0);
             const Agg ag1 = P.lag_aggregate(T2, 1);
             // implicit mode: weights a = -W^-2 G v at this iterate, aggregated like z
@@ -2023,7 +2072,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1) {
             Agg agA0 = ag0, agA1 = ag1;
             bool imp_ok = false;
             if (imp) {
-                double wts[Solver<N, NSOC, OMAX, LPP, BALL, CONE, OE>::M];
+                double wts[Slv::M];
                 imp_ok = P.implicit_weights(wts);
                 agA0 = P.lag_aggregate(T1, 0, wts);
                 agA1 = P.lag_aggregate(T2, 1, wts);
@@ -2127,6 +2176,14 @@ __global__ void __launch_bounds__(kSolveBlock, WPS) prox_kernel(KArgs A) {
     if (slot >= A.n) return;
     const int64_t pi = A.perm ? (int64_t)A.perm[A.slot0 + slot] : (A.slot0 + slot);
     solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0, OE, (FL & 16) ? 1 : 0>(A, pi, q);
+#if defined(__HIP_DEVICE_COMPILE__)
+    // the pair's lanes are in this wave and reconverged here: the fence waits for all of the
+    // wave's stores (the other lanes' gradient entries included) before the flag is released
+    if (A.done && t == 0) {
+        __threadfence_system();
+        __hip_atomic_store(A.done, A.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+#endif
 }
 
 // The resume launch of a suspend / resume pair: one lane group per continuation entry;

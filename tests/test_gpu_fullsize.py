@@ -229,6 +229,70 @@ def test_codegen_invariance_mixed(tmp_path):
     _assert_bitwise(_mixed_outputs(tmp_path, "product"), _mixed_outputs(tmp_path, "xcheck", lib=XCHECK_LIB))
 
 
+_TWIN_EXTRA_SCRIPT = r"""
+import glob, os, sys, numpy as np
+sys.path[:0] = [sys.argv[2], sys.argv[3], os.path.join(sys.argv[3], "tests")]
+from dcol_amd import Engine, spec_from_arrays
+from stress_shapes import random_pairs, random_table
+out = {}
+eng = Engine(device=0)
+# stress shapes: the 48 / 64 / 128-row buckets at 8 / 16 lanes per pair, offsets, polygons
+# with 3-12 edges; the same pairs with the case-4 extension (N = 7 / 8 kernels)
+rng = np.random.default_rng(2)
+tab = random_table(rng)
+s1, s2, p1, p2 = random_pairs(rng, tab, 200_000)
+ids = np.array([eng.register(spec_from_arrays(tab, k)) for k in range(len(tab["type"]))], np.int32)
+for tag, c4 in (("stress", False), ("stress_case4", True)):
+    r = eng.solve_host(ids[s1], ids[s2], p1, p2, grad="fd", contact=True, case4=c4)
+    for k in ("alpha", "grad", "contact", "iters", "status"):
+        out[f"{tag}_{k}"] = getattr(r, k)
+# small plans (fused / latency configurations): every golden file, FD and envelope, the
+# mixed one also with case 4
+for path in sorted(glob.glob(os.path.join(sys.argv[3], "tests", "golden", "*.npz"))):
+    d = dict(np.load(path, allow_pickle=False))
+    if "type" not in d or "tol0" in path:
+        continue
+    gi = np.array([eng.register(spec_from_arrays(d, k)) for k in range(len(d["type"]))], np.int32)
+    name = os.path.basename(path)[:-4]
+    for mode in ("fd", "envelope"):
+        for c4 in ((False, True) if "mixed" in name else (False,)):
+            r = eng.solve_host(gi[d["s1"]], gi[d["s2"]], d["pose1"], d["pose2"], tol=float(d["tol"]), grad=mode,
+                               contact=True, case4=c4)
+            for k in ("alpha", "grad", "contact", "iters", "status"):
+                out[f"{name}_{mode}_{int(c4)}_{k}"] = getattr(r, k)
+np.savez(sys.argv[1], **out)
+"""
+
+
+def _twin_outputs(tmp_path, name, lib=None):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("DCOL_LIB", "DCOL_NO_BALL", "DCOL_NO_CONE", "DCOL_LPP")}
+    if lib:
+        env["DCOL_LIB"] = lib
+    f = str(tmp_path / f"{name}.npz")
+    subprocess.run([sys.executable, "-c", _TWIN_EXTRA_SCRIPT, f, PKG, REPO], check=True, env=env, timeout=300)
+    return dict(np.load(f))
+
+
+@pytest.mark.skipif(not os.path.exists(XCHECK_LIB), reason="lib_xcheck not built (make -C csrc xcheck)")
+def test_codegen_invariance_stress_case4_small_plans(tmp_path):
+    """The codegen-invariance twin (see test_codegen_invariance_mixed) beyond the 1M mixed set:
+    the stress shapes' 48 / 64 / 128-row buckets at 8 / 16 lanes per pair and non-identity
+    offsets (200k pairs), the case-4 N = 7 / 8 kernels on the same pairs, and the small
+    fused / latency plans of every golden file (scenes, synthetic sets, edge cases; FD and
+    envelope gradients): BITWISE equal between the product library and its twin."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    a = _twin_outputs(tmp_path, "product")
+    b = _twin_outputs(tmp_path, "xcheck", lib=XCHECK_LIB)
+    assert set(a) == set(b) and len(a) > 40
+    for k in a:
+        same = (a[k] == b[k]) | (np.isnan(a[k]) & np.isnan(b[k])) if a[k].dtype.kind == "f" else a[k] == b[k]
+        assert np.all(same), (k, int((~same).sum()))
+    assert (a["stress_case4_status"] == 0).mean() > (a["stress_status"] == 0).mean()   # case-4 pairs solved
+
+
 def test_max_size_192m_pairs_position_independent():
     """Maximum-size launch: 192M pairs in ONE plan (192 copies of a 1M batch of the benchmark
     distribution; 18 GB of poses and 18 GB of gradients in HBM, so pose / gradient offsets

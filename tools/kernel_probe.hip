@@ -15,6 +15,10 @@
 
 #include "dcol_host.hpp"
 
+#ifndef DCOL_PROBE_FL
+#define DCOL_PROBE_FL 1   // variants.py FL of the probed copy (1: FULL, as the library launches box x box)
+#endif
+
 using namespace dcol;
 using namespace dcol_host;
 
@@ -94,14 +98,14 @@ int main(int argc, char** argv) {
     const int launches = argc > 2 ? std::atoi(argv[2]) : 500;
     const int warm = argc > 3 ? std::atoi(argv[3]) : 200;
     for (int rep = 0; rep < warm; ++rep)
-        hipLaunchKernelGGL((prox_kernel<4, 0, 12, LPP, 2, 1>), dim3(grid), dim3(kSolveBlock), 0, 0, a);
+        hipLaunchKernelGGL((prox_kernel<4, 0, 12, LPP, 2, DCOL_PROBE_FL>), dim3(grid), dim3(kSolveBlock), 0, 0, a);
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     std::vector<float> ms(launches);
     for (int rep = 0; rep < launches; ++rep) {
         CK(hipEventRecord(e0, 0));
-        hipLaunchKernelGGL((prox_kernel<4, 0, 12, LPP, 2, 1>), dim3(grid), dim3(kSolveBlock), 0, 0, a);
+        hipLaunchKernelGGL((prox_kernel<4, 0, 12, LPP, 2, DCOL_PROBE_FL>), dim3(grid), dim3(kSolveBlock), 0, 0, a);
         CK(hipEventRecord(e1, 0));
         CK(hipEventSynchronize(e1));
         CK(hipEventElapsedTime(&ms[rep], e0, e1));

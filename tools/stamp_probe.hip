@@ -17,6 +17,10 @@
 
 #include "dcol_host.hpp"
 
+#ifndef DCOL_PROBE_FL
+#define DCOL_PROBE_FL 1   // variants.py FL of the probed copy (1: FULL, as the library launches box x box)
+#endif
+
 using namespace dcol;
 using namespace dcol_host;
 
@@ -97,7 +101,7 @@ int main(int argc, char** argv) {
     constexpr int LPP = 2;
     const int64_t grid = (B * LPP + kSolveBlock - 1) / kSolveBlock;
     for (int rep = 0; rep < 3; ++rep) {
-        hipLaunchKernelGGL((prox_kernel<4, 0, 12, LPP, 2, 1>), dim3(grid), dim3(kSolveBlock), 0, 0, a);
+        hipLaunchKernelGGL((prox_kernel<4, 0, 12, LPP, 2, DCOL_PROBE_FL>), dim3(grid), dim3(kSolveBlock), 0, 0, a);
         CK(hipDeviceSynchronize());
     }
     std::vector<unsigned long long> st(16 * B);
