@@ -2176,7 +2176,7 @@ __global__ void __launch_bounds__(kSolveBlock, WPS) prox_kernel(KArgs A) {
     if (slot >= A.n) return;
     const int64_t pi = A.perm ? (int64_t)A.perm[A.slot0 + slot] : (A.slot0 + slot);
     solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0, OE, (FL & 16) ? 1 : 0>(A, pi, q);
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(DCOL_NO_DONE_FLAG)
     // the pair's lanes are in this wave and reconverged here: the fence waits for all of the
     // wave's stores (the other lanes' gradient entries included) before the flag is released
     if (A.done && t == 0) {

@@ -8,7 +8,7 @@ NAME=${1:?name}
 OUT=gpurun_out/$NAME
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-B="python3 bench.py --no-cpu --no-altro --check 0 --steps 200 --warmup 100 --streams 1 --mixed-steps 0"
+B="python3 bench.py --no-cpu --no-altro --check 0 --steps 200 --warmup 100 --streams 1 --mixed-steps 0 --no-kernel-1m"
 M="python3 bench.py --workload mixed1m --no-cpu --no-altro --check 0 --steps 20 --warmup 5"
 tools/gpu_session.sh \
   "tests|600|python3 -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread" \
