@@ -697,9 +697,9 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
     elapsed_serial = timed([step]) if len(lanes) > 1 else None
     elapsed = timed(lanes if len(lanes) > 1 else [step])
 
-    def ev_medians(fns, reps=20):
-        """median HIP-event duration of each fn, the fns interleaved rep by rep (the same clock
-        state for all of them)"""
+    def ev_times(fns, reps=20):
+        """HIP-event durations [reps, len(fns)] (ms), the fns interleaved rep by rep (the same
+        clock state for all of them)"""
         ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in fns]
               for _ in range(reps)]
         for row in ev:
@@ -708,12 +708,16 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
                 fn()
                 e1.record(stream)
         torch.cuda.synchronize(dev)
-        return [float(np.median([row[i][0].elapsed_time(row[i][1]) for row in ev])) for i in range(len(fns))]
+        return np.array([[e0.elapsed_time(e1) for e0, e1 in row] for row in ev])
     # like for like (HIP events on the launch stream, one step at a time, interleaved): solve =
     # the step's own solve and record writes without its collective; step = the same with it;
     # their difference is the communication cost of the step (5-50 %
     # predicted at 8 GPUs).  kernel = the plan run with the per-pair arrays (FP64 roofline).
-    solve_ms, step_ms, kernel_ms = ev_medians([solve_only, step, launch])
+    tt = ev_times([solve_only, step, launch])
+    solve_ms, step_ms, kernel_ms = (float(v) for v in np.median(tt, axis=0))
+    comm_d = tt[:, 1] - tt[:, 0]          # paired: each step against the solve just before it
+    comm_ms = float(np.median(comm_d))
+    comm_iqr = float(np.subtract(*np.percentile(comm_d, [75, 25])))
     my_iters = out["iters"].cpu().numpy()
     my_status = out["status"].cpu().numpy()
     flops_local = mixed_flops(tab, s1[mine], s2[mine], my_iters, my_status, args.grad)
@@ -757,9 +761,11 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
                     "solve = the step's own solve and record writes without its collective (" + (
                         "the plan run with the per-pair arrays; the pack pass + all-gather are the comm"
                         if args.pack_pass else "dcol_prox_batch_multi_gpu with DCOL_NO_GATHER") +
-                    "); step = the same with the all-gather; comm = step - solve",
+                    "); step = the same with the all-gather; comm = the median of the paired per-rep differences "
+                    "step - solve (its interquartile range beside it: the measurement's noise)",
             "solve_ms_max_rank": solve_ms_max, "step_ms_max_rank": float(ranks_stats[:, 1].max()),
-            "comm_ms_rank0": step_ms - solve_ms, "comm_frac_rank0": (step_ms - solve_ms) / step_ms if step_ms > 0 else None,
+            "comm_ms_rank0": comm_ms, "comm_frac_rank0": comm_ms / step_ms if step_ms > 0 else None,
+            "comm_ms_iqr_rank0": comm_iqr,
             "record_bytes_per_pair": REC * 8,
             "per_rank": {"solve_ms": ranks_stats[:, 0].tolist(), "step_ms": ranks_stats[:, 1].tolist(),
                          "kernel_ms": ranks_stats[:, 4].tolist(),

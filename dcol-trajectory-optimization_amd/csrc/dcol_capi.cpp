@@ -66,17 +66,27 @@ DeviceSide& device_side(int dev) {
     static DeviceSide g[64];
     return g[dev & 63];
 }
+// side streams per device: 3 (with the caller's stream, 4 = HIP's default hardware queues),
+// DCOL_SIDE_STREAMS=<1..7> for A/B runs (then raise GPU_MAX_HW_QUEUES to match)
+int side_streams() {
+    static const int n = [] {
+        const char* e = std::getenv("DCOL_SIDE_STREAMS");
+        const int v = e ? std::atoi(e) : 3;
+        return v < 1 ? 1 : (v > kSideStreams ? kSideStreams : v);
+    }();
+    return n;
+}
 bool device_side_streams(int dev, hipStream_t out[kSideStreams]) {
     DeviceSide& d = device_side(dev);
     std::lock_guard<std::mutex> lk(d.mu);
     if (!d.tried) {
         d.tried = true;
         d.ok = true;
-        for (int i = 0; d.ok && i < kSideStreams; ++i) d.ok = hipStreamCreateWithFlags(&d.s[i], hipStreamNonBlocking) == hipSuccess;
+        for (int i = 0; d.ok && i < side_streams(); ++i) d.ok = hipStreamCreateWithFlags(&d.s[i], hipStreamNonBlocking) == hipSuccess;
         if (!d.ok) (void)hipGetLastError();
     }
     if (d.ok)
-        for (int i = 0; i < kSideStreams; ++i) out[i] = d.s[i];
+        for (int i = 0; i < side_streams(); ++i) out[i] = d.s[i];
     return d.ok;
 }
 
@@ -488,7 +498,7 @@ void assign_lanes(dcol_plan* p) {
     p->lanes = 1;
     p->issue.clear();
     if (solves < 2) return;
-    const int lanes = std::min(solves, kSideStreams + 1);
+    const int lanes = std::min(solves, side_streams() + 1);
     std::vector<int> order;
     std::vector<double> cost(p->launches.size(), 0.0);
     for (size_t i = 0; i < p->launches.size(); ++i) {

@@ -7,7 +7,8 @@ namespace dcol {
 // launch flags of a bucket (the variant flags FL of variants.py a launch may use)
 enum : int { LF_FULL = 1, LF_BALL = 2, LF_CONE = 4 };
 constexpr int kBlock = kSolveBlock;   // threads per workgroup of the solve kernel
-constexpr int kSideStreams = 3;   // extra streams for concurrent variant launches (4 HW queues)
+constexpr int kSideStreams = 7;   // capacity of the extra streams for concurrent variant launches
+                                  // (dcol_capi.cpp side_streams(): 3 by default, DCOL_SIDE_STREAMS)
 hipError_t launch_n4(int nsoc, int omax, int lpp, int flags, const KArgs& args, hipStream_t stream);
 hipError_t launch_n5(int nsoc, int omax, int lpp, int flags, const KArgs& args, hipStream_t stream);
 hipError_t launch_n6(int nsoc, int omax, int lpp, int flags, const KArgs& args, hipStream_t stream);
