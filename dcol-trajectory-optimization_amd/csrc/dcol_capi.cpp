@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <list>
@@ -42,12 +43,13 @@ namespace {
 
 struct DeviceGuard {
     int prev = -1;
+    bool switched = false;
     explicit DeviceGuard(int dev) {
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) (void)hipSetDevice(dev);
+        if (prev != dev) switched = hipSetDevice(dev) == hipSuccess;
     }
     ~DeviceGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
+        if (switched && prev >= 0) (void)hipSetDevice(prev);
     }
 };
 
@@ -75,6 +77,17 @@ int side_streams() {
         return v < 1 ? 1 : (v > kSideStreams ? kSideStreams : v);
     }();
     return n;
+}
+
+// dcol_prox_pair's one-pair server: how long (us) it stays resident without a request
+// (DCOL_PAIR_SERVER_IDLE_US, default 1000); DCOL_PAIR_SERVER=0: no server, one launch per
+// call.  Read per call (tests switch it).
+int pair_server_idle_us() {
+    const char* on = std::getenv("DCOL_PAIR_SERVER");
+    if (on && std::atoi(on) == 0) return 0;
+    const char* e = std::getenv("DCOL_PAIR_SERVER_IDLE_US");
+    const long v = e ? std::atol(e) : 1000;
+    return v < 0 ? 0 : (v > 1000000 ? 1000000 : (int)v);
 }
 bool device_side_streams(int dev, hipStream_t out[kSideStreams]) {
     DeviceSide& d = device_side(dev);
@@ -136,15 +149,20 @@ struct dcol_table {
     hipStream_t side[kSideStreams] = {};
     bool side_ready = false;
     // dcol_prox_pair: one-pair plans per (shape1, shape2), at most DCOL_PAIR_PLANS_MAX, least
-    // recently used first out (pair_lru: most recent at the front), a stream, and
-    // device-mapped pinned staging [pose1 (6) | pose2 (6) | alpha | contact (3) | grad (12) |
-    // (iters, status)]
+    // recently used first out (pair_lru: most recent at the front), a stream for their
+    // launches, and the device-mapped pinned mailbox (PairBox: poses, outputs, the request of
+    // the one-pair server and its stream)
     std::list<std::pair<int64_t, dcol_plan*>> pair_lru;
     std::unordered_map<int64_t, std::list<std::pair<int64_t, dcol_plan*>>::iterator> pair_plans;
     hipStream_t pair_stream = nullptr;
-    double* pair_host = nullptr;
-    double* pair_dev = nullptr;
-    int32_t pair_seq = 0;   // completion flag value of the last one-pair launch
+    hipStream_t server_stream = nullptr;
+    PairBox* pair_host = nullptr;
+    PairBox* pair_dev = nullptr;
+    int32_t pair_seq = 0;          // completion flag value of the last one-pair launch
+    int64_t wall_ticks_us = 0;     // device wall-clock ticks per microsecond (0: unknown, no server)
+    bool server_launched = false;  // a server was launched at least once (destroy stops it)
+    int64_t n_served = 0, n_launched = 0, n_starts = 0;   // dcol_table_pair_stats
+    double srv_us = 0.0, srv_cycles = 0.0;
 };
 
 struct Launch {
@@ -281,8 +299,13 @@ int dcol_table_create(const dcol_shape_desc* shapes, int32_t n, int32_t device, 
 int dcol_table_destroy(dcol_table* t) {
     if (!t) return DCOL_SUCCESS;
     DeviceGuard g(t->device);
+    if (t->server_launched) {   // the server exits at its next poll
+        __atomic_store_n(&t->pair_host->stop, 1, __ATOMIC_SEQ_CST);
+        (void)hipStreamSynchronize(t->server_stream);
+    }
     for (auto& kv : t->pair_lru) dcol_plan_destroy(kv.second);
     if (t->pair_stream) (void)hipStreamDestroy(t->pair_stream);
+    if (t->server_stream) (void)hipStreamDestroy(t->server_stream);
     if (t->pair_host) (void)hipHostFree(t->pair_host);
     if (t->d_shapes) (void)hipFree(t->d_shapes);
     if (t->d_rows) (void)hipFree(t->d_rows);
@@ -881,19 +904,26 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
     dcol_table* t = const_cast<dcol_table*>(tc);
     std::lock_guard<std::mutex> lk(t->mu);
     DeviceGuard g(t->device);
-    constexpr int kSlots = 12 + 1 + 3 + 12 + 1 + 1;   // ... | (iters, status) | completion flag
     if (!t->pair_host) {
-        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&t->pair_host), kSlots * sizeof(double),
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&t->pair_host), sizeof(PairBox),
                                      hipHostMallocMapped | hipHostMallocPortable);
-        if (e == hipSuccess) std::memset(t->pair_host, 0, kSlots * sizeof(double));   // the flag word starts at 0
+        if (e == hipSuccess) std::memset(t->pair_host, 0, sizeof(PairBox));   // flags and sequence numbers start at 0
         if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&t->pair_dev), t->pair_host, 0);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&t->pair_stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&t->server_stream, hipStreamNonBlocking);
+        int khz = 0;
+        if (e == hipSuccess && hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, t->device) != hipSuccess) {
+            (void)hipGetLastError();
+            khz = 0;
+        }
         if (e != hipSuccess) {
             if (t->pair_host) (void)hipHostFree(t->pair_host);
+            if (t->pair_stream) (void)hipStreamDestroy(t->pair_stream);
             t->pair_host = t->pair_dev = nullptr;
             t->pair_stream = nullptr;
             return fail(DCOL_ERR_HIP, std::string("dcol_prox_pair staging: ") + hipGetErrorString(e));
         }
+        t->wall_ticks_us = khz > 0 ? (int64_t)khz / 1000 : 0;
     }
     const int64_t key = (int64_t)s1 * ns + s2;
     const bool c4 = (flags & DCOL_CASE4) != 0;
@@ -916,26 +946,123 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
         t->pair_lru.emplace_front(ck, plan);
         t->pair_plans.emplace(ck, t->pair_lru.begin());
     }
-    double* h = t->pair_host;
-    double* d = t->pair_dev;
-    std::memcpy(h, pose1, 6 * sizeof(double));
-    std::memcpy(h + 6, pose2, 6 * sizeof(double));
-    int32_t* hi = reinterpret_cast<int32_t*>(h + 28);
-    int32_t* di = reinterpret_cast<int32_t*>(d + 28);
+    PairBox* h = t->pair_host;
+    PairBox* d = t->pair_dev;
+    std::memcpy(h->pose1, pose1, 6 * sizeof(double));
+    std::memcpy(h->pose2, pose2, 6 * sizeof(double));
     // SoA of one pair = the 6 values in order; the kernel reads / writes the mapped memory.
-    // Completion: a one-launch solve plan releases a sequence number into the mapped flag
-    // word after its output stores (KArgs::done), and this thread polls host memory for it
-    // -- no stream synchronisation on the latency path; the stream is queried now and then,
-    // so a launch that ends without the flag (or fails) is still caught.  Other plans (a
-    // rejected pair) synchronise the stream.
-    volatile int32_t* hflag = reinterpret_cast<volatile int32_t*>(h + 29);
-    int32_t* dflag = reinterpret_cast<int32_t*>(d + 29);
     const bool flagged = plan->launches.size() == 1 && plan->launches[0].kind == 0 && !plan->fused() &&
                          !plan->launches[0].susp && plan->lanes <= 1;
+    // The one-pair server (PairBox, prox_fused_kernel): a resident workgroup of the fused
+    // kernel polls the mailbox, so a call whose variant the fused kernel has costs no launch.
+    const int idle_us = pair_server_idle_us();
+    const Launch& L0 = plan->launches[0];
+    const int vid = (flagged && idle_us > 0 && t->wall_ticks_us > 0 && ns <= (1 << kPairBoxIdBits) && L0.lpp < 65536)
+                        ? fused_vid(L0.N, L0.nsoc, L0.omax, L0.lpp, L0.flags(), L0.oe) : -1;
+    if (vid >= 0) {
+        const int32_t kflags = flags & ~DCOL_CASE4;
+        const auto start_server = [&]() -> hipError_t {
+            KArgs a;
+            a.shapes = t->d_shapes;
+            a.rows = t->d_rows;
+            a.s1 = nullptr;   // the shape ids come with each request (PairBox::ids)
+            a.s2 = nullptr;
+            a.pose1 = d->pose1;
+            a.pose2 = d->pose2;
+            a.perm = nullptr;
+            a.B = 1;
+            a.slot0 = 0;
+            a.n = 1;
+            a.tol = tol;
+            a.max_iter = max_iter;
+            a.flags = kflags;
+            a.alpha = &d->alpha;
+            a.contact = d->contact;
+            a.grad = d->grad;
+            a.iters = &d->iters;
+            a.status = &d->status;
+            a.rec = nullptr;
+            a.susp_t = 0;
+            a.susp_min = 0;
+            a.susp_count = nullptr;
+            a.susp_pi = nullptr;
+            a.susp_state = nullptr;
+            a.susp_cap = 0;
+            h->flags = kflags;
+            h->tol = tol;
+            h->max_iter = max_iter;
+            t->server_launched = true;
+            ++t->n_starts;
+            return launch_pair_server(a, d, (int64_t)idle_us * t->wall_ticks_us, t->server_stream);
+        };
+        // flags / tolerance / iteration cap are the server's launch arguments: a call with
+        // others stops the running server first (an ALTRO loop switches between
+        // proximity_mrp and proximity_gradient per phase, not per call)
+        if (t->server_launched && (h->flags != kflags || h->tol != tol || h->max_iter != max_iter)) {
+            __atomic_store_n(&h->stop, 1, __ATOMIC_SEQ_CST);
+            const hipError_t e = hipStreamSynchronize(t->server_stream);
+            __atomic_store_n(&h->stop, 0, __ATOMIC_SEQ_CST);
+            __atomic_store_n(&h->alive, 0, __ATOMIC_SEQ_CST);
+            if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_prox_pair server: ") + hipGetErrorString(e));
+        }
+        const uint32_t useq = (uint32_t)(h->req >> 32) + 1u;
+        const int32_t seq = (int32_t)useq;
+        h->ids = ((uint64_t)(useq & 0xffffu) << 48) | ((uint64_t)(uint32_t)s2 << kPairBoxIdBits) | (uint64_t)(uint32_t)s1;
+        __atomic_store_n(&h->req, ((uint64_t)useq << 32) | ((uint64_t)(uint32_t)L0.lpp << 16) | (uint64_t)(uint32_t)vid,
+                         __ATOMIC_SEQ_CST);
+        // a server that cleared `alive` before this request re-checks `req` on its way out
+        // (and serves it), or it is gone: then start one (a redundant one queues behind the
+        // old one on the server stream, finds nothing to do and leaves after the idle time)
+        if (__atomic_load_n(&h->alive, __ATOMIC_SEQ_CST) == 0) {
+            const hipError_t e = start_server();
+            if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_prox_pair server: ") + hipGetErrorString(e));
+        }
+        int restarts = 0;
+        const auto t_post = std::chrono::steady_clock::now();
+        for (uint64_t spin = 1;; ++spin) {
+            if (__atomic_load_n(&h->done, __ATOMIC_ACQUIRE) == seq) break;
+            if ((spin & 4095) == 0) {   // a failed server surfaces here; an idle stream with the request
+                const hipError_t q = hipStreamQuery(t->server_stream);   // unserved gets a new server
+                if (q == hipErrorNotReady && std::chrono::steady_clock::now() - t_post > std::chrono::seconds(30)) {
+                    // a server that never answers (not expected: a solve takes microseconds):
+                    // make it leave, so the next call starts clean, and report
+                    __atomic_store_n(&h->stop, 1, __ATOMIC_SEQ_CST);
+                    (void)hipStreamSynchronize(t->server_stream);
+                    __atomic_store_n(&h->stop, 0, __ATOMIC_SEQ_CST);
+                    __atomic_store_n(&h->alive, 0, __ATOMIC_SEQ_CST);
+                    return fail(DCOL_ERR_HIP, "dcol_prox_pair: the pair server did not answer within 30 s");
+                }
+                if (q == hipSuccess && __atomic_load_n(&h->done, __ATOMIC_ACQUIRE) != seq) {
+                    const hipError_t e = ++restarts > 2 ? hipErrorLaunchFailure : start_server();
+                    if (e != hipSuccess)
+                        return fail(DCOL_ERR_HIP, std::string("dcol_prox_pair server: ") + hipGetErrorString(e));
+                } else if (q != hipSuccess && q != hipErrorNotReady) {
+                    return fail(DCOL_ERR_HIP, std::string("dcol_prox_pair server: ") + hipGetErrorString(q));
+                }
+            }
+        }
+        ++t->n_served;
+        t->srv_us += (double)h->solve_ticks / (double)t->wall_ticks_us;
+        t->srv_cycles += (double)h->solve_cycles;
+        *alpha = h->alpha;
+        if (contact && (flags & DCOL_CONTACT)) std::memcpy(contact, h->contact, 3 * sizeof(double));
+        if (grad && (flags & DCOL_GRAD_ANY)) std::memcpy(grad, h->grad, 12 * sizeof(double));
+        if (iters) *iters = h->iters;
+        if (status) *status = h->status;
+        return DCOL_SUCCESS;
+    }
+    // Otherwise one launch.  Completion: a one-launch solve plan releases a sequence number
+    // into the mapped flag word after its output stores (KArgs::done), and this thread polls
+    // host memory for it -- no stream synchronisation on the latency path; the stream is
+    // queried now and then, so a launch that ends without the flag (or fails) is still
+    // caught.  Other plans (a rejected pair) synchronise the stream.
+    volatile int32_t* hflag = &h->launch_done;
+    int32_t* dflag = &d->launch_done;
     const int32_t seq = flagged ? (t->pair_seq = t->pair_seq % 0x7ffffffe + 1) : 0;   // 1 .. 2^31 - 2, never 0
-    int rc = plan_run_rec(plan, d, d + 6, tol, max_iter, flags & ~DCOL_CASE4, d + 12, d + 13, d + 16, di, di + 1,
-                          nullptr, t->pair_stream, flagged ? dflag : nullptr, seq);
+    int rc = plan_run_rec(plan, d->pose1, d->pose2, tol, max_iter, flags & ~DCOL_CASE4, &d->alpha, d->contact,
+                          d->grad, &d->iters, &d->status, nullptr, t->pair_stream, flagged ? dflag : nullptr, seq);
     if (rc != DCOL_SUCCESS) return rc;
+    ++t->n_launched;
     if (flagged) {
         bool seen = false;
         for (uint64_t spin = 1;; ++spin) {
@@ -957,11 +1084,11 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
         const hipError_t e = hipStreamSynchronize(t->pair_stream);
         if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_prox_pair: ") + hipGetErrorString(e));
     }
-    *alpha = h[12];
-    if (contact && (flags & DCOL_CONTACT)) std::memcpy(contact, h + 13, 3 * sizeof(double));
-    if (grad && (flags & DCOL_GRAD_ANY)) std::memcpy(grad, h + 16, 12 * sizeof(double));
-    if (iters) *iters = hi[0];
-    if (status) *status = hi[1];
+    *alpha = h->alpha;
+    if (contact && (flags & DCOL_CONTACT)) std::memcpy(contact, h->contact, 3 * sizeof(double));
+    if (grad && (flags & DCOL_GRAD_ANY)) std::memcpy(grad, h->grad, 12 * sizeof(double));
+    if (iters) *iters = h->iters;
+    if (status) *status = h->status;
     return DCOL_SUCCESS;
 }
 
@@ -970,6 +1097,19 @@ int dcol_table_pair_plans(const dcol_table* tc, int32_t* n) {
     dcol_table* t = const_cast<dcol_table*>(tc);
     std::lock_guard<std::mutex> lk(t->mu);
     *n = (int32_t)t->pair_lru.size();
+    return DCOL_SUCCESS;
+}
+
+int dcol_table_pair_stats(const dcol_table* tc, int64_t* served, int64_t* launched, int64_t* server_starts,
+                          double* server_solve_us, double* server_solve_cycles) {
+    if (!tc) return fail(DCOL_ERR_ARG, "dcol_table_pair_stats: NULL table");
+    dcol_table* t = const_cast<dcol_table*>(tc);
+    std::lock_guard<std::mutex> lk(t->mu);
+    if (served) *served = t->n_served;
+    if (launched) *launched = t->n_launched;
+    if (server_starts) *server_starts = t->n_starts;
+    if (server_solve_us) *server_solve_us = t->srv_us;
+    if (server_solve_cycles) *server_solve_cycles = t->srv_cycles;
     return DCOL_SUCCESS;
 }
 

@@ -1994,10 +1994,11 @@ DCOL_HD void launder(P& p) {
 // resume launch, for continuation entry ci (pi = its pair)
 template <int N, int NSOC, int OMAX, int LPP, bool FULL = false, bool BALL = false, bool CONE = false, int OE = 0,
           int MODE = 0>
-DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1) {
+DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1, int k1o = -1, int k2o = -1) {
     DCOL_STAMP(A, pi, q, 0);
     const int64_t B = A.B;
-    const int k1 = A.s1[pi], k2 = A.s2[pi];
+    // k1o / k2o >= 0: the shape ids given (the one-pair server reads them with its request)
+    const int k1 = k1o >= 0 ? k1o : A.s1[pi], k2 = k2o >= 0 ? k2o : A.s2[pi];
     const DevShape& S1 = A.shapes[k1];
     const DevShape& S2 = A.shapes[k2];
     double th1[6], th2[6];

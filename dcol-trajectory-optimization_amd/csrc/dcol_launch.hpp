@@ -35,6 +35,35 @@ hipError_t launch_susp(int N, int nsoc, int omax, int lpp, int flags, int oe, co
 // the fused kernel lacks it
 int fused_vid(int N, int nsoc, int omax, int lpp, int flags, int oe = 0);
 hipError_t launch_fused(const KArgs& args, const FusedSeg* d_segs, int nseg, int64_t blocks, hipStream_t stream);
+
+// Mailbox of the one-pair server (dcol_prox_pair; dcol_kernels_server.hip prox_pair_server):
+// device-mapped pinned host memory, one per table.  The caller writes the poses and the
+// shape-id word, then releases the request word: a new sequence number in its high half,
+// the pair's fused variant id and lanes in its low half, so one poll of the server reads
+// all it needs to branch.  The id word carries the sequence number's low 16 bits: the server
+// loads it together with the request word (one round trip) and re-reads it only if it saw
+// an older one.  The server solves the pair into the output slots and releases the sequence
+// number into `done`.  `alive` is 1 while a server polls (it clears it before it exits and
+// then re-checks the request word, so a request posted meanwhile is either served or seen by
+// the caller as "start a server"); `stop` makes it exit at its next poll.  flags / tol /
+// max_iter: those of the running server (a call with others restarts it).
+struct PairBox {
+    double pose1[6], pose2[6];
+    double alpha, contact[3], grad[12];
+    int32_t iters, status;
+    double tol;
+    int32_t flags, max_iter;
+    uint64_t req;   // seq << 32 | lpp << 16 | vid
+    uint64_t ids;   // (seq & 0xffff) << 48 | s2 << 24 | s1   (shape ids below 2^24)
+    int32_t done, alive, stop;
+    int32_t launch_done;   // completion flag of a one-pair launch outside the server (KArgs::done)
+    int64_t solve_ticks, solve_cycles;   // the last served request: wall-clock ticks and shader cycles
+};
+constexpr int kPairBoxIdBits = 24;
+// a server on `stream` serving box (device view) with args' table pointers, flags, tolerance
+// and iteration cap; it exits after idle_ticks of the device wall clock
+// (hipDeviceAttributeWallClockRate) without a request
+hipError_t launch_pair_server(const KArgs& args, PairBox* box, int64_t idle_ticks, hipStream_t stream);
 #ifdef DCOL_CHECK_EXEC
 // diagnostic build: host reader of a translation unit's DPP-source violation counter
 // (dcol_device.hpp dpp_check), summed by dcol_debug_exec_violations (dcol_capi.cpp)
@@ -46,7 +75,7 @@ hipError_t launch_fused(const KArgs& args, const FusedSeg* d_segs, int nseg, int
         if (reset) (void)hipMemcpyToSymbol(HIP_SYMBOL(dcol_exec_violations), &z, sizeof(z));   \
         return v;                                                                              \
     }
-#define DCOL_EXEC_TAGS(X) X(n4) X(n5) X(n6) X(n7) X(n8) X(fused) X(p51) X(p52) X(p61) X(p62) X(susp)
+#define DCOL_EXEC_TAGS(X) X(n4) X(n5) X(n6) X(n7) X(n8) X(fused) X(p51) X(p52) X(p61) X(p62) X(susp) X(server)
 #define DCOL_EXEC_DECL(tag) unsigned long long exec_violations_##tag(bool reset);
 DCOL_EXEC_TAGS(DCOL_EXEC_DECL)
 DCOL_EXEC_DECL(capi)   // the C-ABI unit's own counter (dcol_debug_exec_selftest)

@@ -345,6 +345,21 @@ class Engine:
         engine lock from the pose writes to the output copies (two threads on the default
         engine would otherwise overwrite each other's poses or outputs)."""
         flags = grad_flag(grad) | (_lib.CONTACT if contact else 0)
+        # fast path (csrc/fastpair.c): both objects known and the table built -- the poses,
+        # the library call and the outputs in one C function, no engine lock needed (the
+        # library serialises calls per table; `table` keeps this table alive for the call)
+        table = self._table
+        if table is not None:   # (the library is loaded only once a table exists)
+            h1 = self._obj_ids.get(id(prim1))
+            h2 = self._obj_ids.get(id(prim2))
+            fast = _fastpair()
+            if fast is not None and h1 is not None and h2 is not None and h1[0] is prim1 and h2[0] is prim2:
+                r = fast[0](fast[1], table.handle.value, h1[1], h2[1], prim1.r, prim1.p, prim2.r, prim2.p, tol,
+                            self.max_iter, flags, contact)
+                if r is not None:
+                    if r[0]:
+                        _lib.check(r[0], "dcol_prox_pair")
+                    return r[1:]
         with self._lock:
             s1 = self.register_object(prim1)
             s2 = self.register_object(prim2)
@@ -364,6 +379,34 @@ class Engine:
                 _lib.check(rc, "dcol_prox_pair")
             return (np.float64(alpha[0]), cp.copy() if contact else None, g.copy() if flags & _lib.GRAD_ANY else None,
                     int(ints[0]), int(ints[1]))
+
+    def pair_stats(self):
+        """dcol_table_pair_stats of the current table: {"served": calls the one-pair server
+        answered, "launched": calls that launched their own kernel, "server_starts",
+        "server_solve_us" / "server_solve_cycles": device time from request to answer summed
+        over the served calls}."""
+        with self._lock:
+            v = [ctypes.c_int64() for _ in range(3)] + [ctypes.c_double() for _ in range(2)]
+            _lib.check(_lib.load().dcol_table_pair_stats(self.table.handle, *[ctypes.byref(x) for x in v]),
+                       "dcol_table_pair_stats")
+            keys = ("served", "launched", "server_starts", "server_solve_us", "server_solve_cycles")
+            return {k: x.value for k, x in zip(keys, v)}
+
+
+_fast = None
+
+
+def _fastpair():
+    """(dcol_amd._fastpair.solve, address of dcol_prox_pair) or None when the extension is
+    not built (Engine.solve_pair then stages through ctypes: same library call)"""
+    global _fast
+    if _fast is None:
+        try:
+            from . import _fastpair as fp
+            _fast = (fp.solve, ctypes.cast(_lib.load().dcol_prox_pair, ctypes.c_void_p).value)
+        except ImportError:
+            _fast = False
+    return _fast or None
 
 
 _default: Engine | None = None

@@ -38,7 +38,8 @@ extern "C" {
 #endif
 
 #define DCOL_ABI_VERSION 3   /* 2: 14-slot multi-GPU record (status / iters as an int32 pair);
-                                3: DCOL_NO_GATHER + dcol_comm_all_gather, dcol_table_pair_plans */
+                                3: DCOL_NO_GATHER + dcol_comm_all_gather, dcol_table_pair_plans,
+                                   dcol_table_pair_stats */
 
 /* Primitive types (misc_primitive_constructor.py:4-88). */
 enum dcol_shape_type {
@@ -191,8 +192,13 @@ int dcol_prox_batch_host(const dcol_table* table, int64_t B, const int32_t* shap
  * systems/cluttered_hallway_quadrotor.py:131-133, :155).  HOST arguments: pose1/pose2 (6),
  * contact (3, if DCOL_CONTACT, else may be NULL), grad (12, if a GRAD flag, else may be NULL),
  * iters / status (may be NULL).  Synchronous.  Latency path: a one-pair plan cached per
- * (shape1, shape2) in the table, poses and outputs in device-mapped pinned host memory read
- * and written by the kernel itself (no copy commands), one launch on a stream of the table.
+ * (shape1, shape2) in the table (its kernel variant), poses and outputs in device-mapped
+ * pinned host memory read and written by the GPU itself (no copy commands).  A pair whose
+ * variant the fused small-plan kernel has is served by the table's one-pair SERVER: one
+ * resident workgroup polling that memory, started by the first such call and leaving after
+ * DCOL_PAIR_SERVER_IDLE_US (default 1000) without a request -- no kernel launch per call.
+ * (A device-wide synchronisation issued meanwhile waits for it to leave.)  Other pairs,
+ * and every pair under DCOL_PAIR_SERVER=0, take one launch on a stream of the table.
  * Calls on one table are serialised.                                                      */
 int dcol_prox_pair(const dcol_table* table, int32_t shape1, int32_t shape2, const double* pose1,
                    const double* pose2, double tol, int32_t max_iter, int32_t flags, double* alpha,
@@ -201,6 +207,12 @@ int dcol_prox_pair(const dcol_table* table, int32_t shape1, int32_t shape2, cons
  * so device memory stays bounded however many distinct shape pairs a caller queries).  */
 #define DCOL_PAIR_PLANS_MAX 64
 int dcol_table_pair_plans(const dcol_table* table, int32_t* n);
+/* Counters of dcol_prox_pair on this table: calls answered by the server, calls that
+ * launched their own kernel, server starts, and over the served calls the device time from
+ * the server seeing a request to its answer: microseconds and shader-clock cycles (sums;
+ * their ratio is the clock the solves ran at).  Any pointer may be NULL.                 */
+int dcol_table_pair_stats(const dcol_table* table, int64_t* served, int64_t* launched,
+                          int64_t* server_starts, double* server_solve_us, double* server_solve_cycles);
 
 /* ---- multi-GPU ------------------------------------------------------
  * One process per GPU.  Pairs are independent, so each rank solves its own shard with its

@@ -217,3 +217,78 @@ def test_pose_and_shape_ownership(engine):
     default_engine().forget(ball)
     a4, _ = proximity_mrp(ball, box)
     assert abs(a4 - 2.5) < 1e-5                                         # 5 / (1.5 + 0.5)
+
+
+def _bits(results):
+    """(alpha, contact, grad, iters, status) tuples -> one uint64 array (NaN-exact)"""
+    rows = []
+    for a, cp, g, it, st in results:
+        rows.append(np.concatenate([[a], cp if cp is not None else [], g if g is not None else [],
+                                    [float(it), float(st)]]))
+    return np.array(rows).view(np.uint64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("idle_us", [1000, 20])
+def test_pair_server_bitwise_launch_path(engine, monkeypatch, idle_us):
+    """dcol_prox_pair's one-pair server (csrc/dcol_kernels_server.hip: one resident workgroup
+    polling a device-mapped mailbox, no launch per call) returns bitwise what one launch per
+    call returns (DCOL_PAIR_SERVER=0), for pairs of every golden scene / mixed / edge set,
+    with proximity_mrp's flags and proximity_gradient's (fd and envelope: a flag change
+    restarts the server).  idle 20 us: the server leaves between most calls, so its exit /
+    restart handshake runs hundreds of times; 1000 us: it stays resident (no restarts)."""
+    monkeypatch.setenv("DCOL_PAIR_SERVER_IDLE_US", str(idle_us))
+    for name in ("scene_quad", "scene_cone", "scene_piano", "synthetic_mixed", "edge_cases"):
+        d = load_golden(GOLDEN[name])
+        objs = objects_from_golden(d)
+        tol = float(d["tol"])
+        idx = spread(np.arange(d["s1"].size), 60)
+        for i in idx:                                 # register every shape first (table fixed below)
+            engine.solve_pair(*pose_pair(objs, d, i), tol, grad=None)
+        for grad in (None, "fd", "envelope"):
+            res = {}
+            for server in ("1", "0"):
+                monkeypatch.setenv("DCOL_PAIR_SERVER", server)
+                s0 = engine.pair_stats()
+                res[server] = [engine.solve_pair(*pose_pair(objs, d, i), tol, grad=grad, contact=True) for i in idx]
+                s1 = engine.pair_stats()
+                if server == "1":    # the supported pairs went through the server
+                    assert s1["served"] - s0["served"] >= int(np.sum(d["status"][idx] == 0)) // 2, (name, s0, s1)
+                else:
+                    assert s1["served"] == s0["served"]
+            np.testing.assert_array_equal(_bits(res["1"]), _bits(res["0"]), err_msg=f"{name} grad={grad}")
+            st = np.array([r[4] for r in res["1"]])
+            np.testing.assert_array_equal(st, d["status"][idx])
+
+
+@pytest.mark.gpu
+def test_pair_server_idle_exit_and_restart(engine, monkeypatch):
+    """The server leaves after its idle time (the stream drains: a device synchronise
+    returns) and the next call starts a new one; alternating mrp / gradient calls restart it
+    per call and stay bitwise equal to the first answers."""
+    import time
+
+    import torch
+    from primitives.misc_primitive_constructor import SphereMRP, create_rect_prism
+    monkeypatch.setenv("DCOL_PAIR_SERVER", "1")
+    monkeypatch.setenv("DCOL_PAIR_SERVER_IDLE_US", "200")
+    box = create_rect_prism(1.0, 2.0, 0.5)
+    ball = SphereMRP(0.4)
+    box.r, box.p = np.zeros(3), np.array([0.1, -0.2, 0.3])
+    ball.r, ball.p = np.array([2.0, 0.5, -0.3]), np.zeros(3)
+    ref_m = engine.solve_pair(ball, box, grad=None)
+    ref_g = engine.solve_pair(ball, box, grad="fd")
+    s0 = engine.pair_stats()
+    for k in range(20):
+        m = engine.solve_pair(ball, box, grad=None)
+        g = engine.solve_pair(ball, box, grad="fd")
+        np.testing.assert_array_equal(_bits([m]), _bits([ref_m]))
+        np.testing.assert_array_equal(_bits([g]), _bits([ref_g]))
+        if k % 5 == 4:
+            time.sleep(0.002)                         # > the idle time: the server has left
+            t0 = time.perf_counter()
+            torch.cuda.synchronize()
+            assert time.perf_counter() - t0 < 0.5
+    s1 = engine.pair_stats()
+    assert s1["served"] - s0["served"] == 40
+    assert s1["server_starts"] - s0["server_starts"] >= 40   # every flag change restarts it
