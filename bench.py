@@ -845,11 +845,15 @@ def dropin_section(reps=3):
     nx = int(params["nx"])
     Xr = np.asarray(params["Xref"], dtype=np.float64).reshape(-1, nx)
     out = {"pattern": f"{len(Xr)} knots x {len(obs)} obstacles of the quadrotor hallway, one call per pair "
-                      "(P_vic.r / .p overwritten per knot)", "calls_per_sweep": len(Xr) * len(obs)}
+                      "(P_vic.r / .p overwritten per knot)", "calls_per_sweep": len(Xr) * len(obs),
+           "path": "dcol_prox_pair: resident one-pair server (DCOL_PAIR_SERVER=0: one launch per call), "
+                   "host glue dcol_amd._fastpair"}
+    from dcol_amd.engine import default_engine
     for name, fn in (("proximity_mrp", proximity_mrp), ("proximity_gradient", proximity_gradient)):
         for o in obs:                     # first call per pair kind: its plan, code objects
             vic.r, vic.p = np.array(Xr[0, 0:3]), np.array(Xr[0, 6:9])
             fn(vic, o)
+        s0 = default_engine().pair_stats()
         best = None
         for _ in range(reps):
             t0 = time.perf_counter()
@@ -860,7 +864,12 @@ def dropin_section(reps=3):
                     fn(vic, o)
             dt = time.perf_counter() - t0
             best = dt if best is None else min(best, dt)
-        out[name] = {"us_per_call": 1e6 * best / (len(Xr) * len(obs))}
+        s1 = default_engine().pair_stats()
+        served = s1["served"] - s0["served"]
+        out[name] = {"us_per_call": 1e6 * best / (len(Xr) * len(obs)), "served_by_pair_server": served,
+                     "launched": s1["launched"] - s0["launched"]}
+        if served:   # the resident one-pair server's request-to-answer time on the device
+            out[name]["device_us_per_call"] = (s1["server_solve_us"] - s0["server_solve_us"]) / served
     t_mrp, t_grad = out["proximity_mrp"]["us_per_call"], out["proximity_gradient"]["us_per_call"]
     proj = ((QUAD_SOLVES - QUAD_GRAD_CALLS) * t_mrp + QUAD_GRAD_CALLS * t_grad) * 1e-6
     out["projected_quadrotor_altro"] = {

@@ -158,7 +158,6 @@ struct dcol_table {
     hipStream_t server_stream = nullptr;
     PairBox* pair_host = nullptr;
     PairBox* pair_dev = nullptr;
-    int32_t pair_seq = 0;          // completion flag value of the last one-pair launch
     int64_t wall_ticks_us = 0;     // device wall-clock ticks per microsecond (0: unknown, no server)
     bool server_launched = false;  // a server was launched at least once (destroy stops it)
     int64_t n_served = 0, n_launched = 0, n_starts = 0;   // dcol_table_pair_stats
@@ -794,10 +793,9 @@ int dcol_plan_bucket(const dcol_plan* p, int32_t i, int32_t info[8], int64_t* pa
 namespace {
 // dcol_plan_run with an optional record output (rec: [B][DCOL_REC], written by the solver
 // epilogues; then alpha / grad / iters / status may be NULL)
-// done / done_seq: completion flag of a one-pair plan (dcol_prox_pair; KArgs::done)
 int plan_run_rec(const dcol_plan* p, const double* pose1, const double* pose2, double tol, int32_t max_iter,
                  int32_t flags, double* alpha, double* contact, double* grad, int32_t* iters, int32_t* status,
-                 double* rec, void* stream, int32_t* done = nullptr, int32_t done_seq = 0) {
+                 double* rec, void* stream) {
     if (!p) return fail(DCOL_ERR_ARG, "dcol_plan_run: NULL plan");
     if (p->B == 0) return DCOL_SUCCESS;
     if (!pose1 || !pose2 || (!alpha && !rec))
@@ -832,8 +830,6 @@ int plan_run_rec(const dcol_plan* p, const double* pose1, const double* pose2, d
     a.susp_pi = nullptr;
     a.susp_state = nullptr;
     a.susp_cap = 0;
-    a.done = done;
-    a.done_seq = done_seq;
     const bool fan = p->lanes > 1 && p->fork;
     hipError_t e = hipSuccess;
     if (fan) {
@@ -951,13 +947,14 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
     std::memcpy(h->pose1, pose1, 6 * sizeof(double));
     std::memcpy(h->pose2, pose2, 6 * sizeof(double));
     // SoA of one pair = the 6 values in order; the kernel reads / writes the mapped memory.
-    const bool flagged = plan->launches.size() == 1 && plan->launches[0].kind == 0 && !plan->fused() &&
+    const bool single = plan->launches.size() == 1 && plan->launches[0].kind == 0 && !plan->fused() &&
                          !plan->launches[0].susp && plan->lanes <= 1;
-    // The one-pair server (PairBox, prox_fused_kernel): a resident workgroup of the fused
-    // kernel polls the mailbox, so a call whose variant the fused kernel has costs no launch.
+    // The one-pair server (PairBox, dcol_kernels_server.hip): a resident workgroup polls the
+    // mailbox, so a call whose variant the fused kernel has (the server switches over the
+    // same solver copies) costs no launch.
     const int idle_us = pair_server_idle_us();
     const Launch& L0 = plan->launches[0];
-    const int vid = (flagged && idle_us > 0 && t->wall_ticks_us > 0 && ns <= (1 << kPairBoxIdBits) && L0.lpp < 65536)
+    const int vid = (single && idle_us > 0 && t->wall_ticks_us > 0 && ns <= (1 << kPairBoxIdBits) && L0.lpp < 65536)
                         ? fused_vid(L0.N, L0.nsoc, L0.omax, L0.lpp, L0.flags(), L0.oe) : -1;
     if (vid >= 0) {
         const int32_t kflags = flags & ~DCOL_CASE4;
@@ -1051,39 +1048,16 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
         if (status) *status = h->status;
         return DCOL_SUCCESS;
     }
-    // Otherwise one launch.  Completion: a one-launch solve plan releases a sequence number
-    // into the mapped flag word after its output stores (KArgs::done), and this thread polls
-    // host memory for it -- no stream synchronisation on the latency path; the stream is
-    // queried now and then, so a launch that ends without the flag (or fails) is still
-    // caught.  Other plans (a rejected pair) synchronise the stream.
-    volatile int32_t* hflag = &h->launch_done;
-    int32_t* dflag = &d->launch_done;
-    const int32_t seq = flagged ? (t->pair_seq = t->pair_seq % 0x7ffffffe + 1) : 0;   // 1 .. 2^31 - 2, never 0
+    // Otherwise one launch on the pair stream, synchronised.  (A completion flag released by
+    // the kernel and polled here saved ~2.5 us per call, but its epilogue cost the one-lane
+    // row-partitioned x polytope kernels 4-5 % of throughput; the server serves the latency
+    // path now.)
     int rc = plan_run_rec(plan, d->pose1, d->pose2, tol, max_iter, flags & ~DCOL_CASE4, &d->alpha, d->contact,
-                          d->grad, &d->iters, &d->status, nullptr, t->pair_stream, flagged ? dflag : nullptr, seq);
+                          d->grad, &d->iters, &d->status, nullptr, t->pair_stream);
     if (rc != DCOL_SUCCESS) return rc;
     ++t->n_launched;
-    if (flagged) {
-        bool seen = false;
-        for (uint64_t spin = 1;; ++spin) {
-            if (__atomic_load_n(const_cast<int32_t*>(hflag), __ATOMIC_ACQUIRE) == seq) {
-                seen = true;
-                break;
-            }
-            if ((spin & 4095) == 0) {
-                const hipError_t q = hipStreamQuery(t->pair_stream);
-                if (q == hipSuccess) {
-                    seen = __atomic_load_n(const_cast<int32_t*>(hflag), __ATOMIC_ACQUIRE) == seq;
-                    break;
-                }
-                if (q != hipErrorNotReady) return fail(DCOL_ERR_HIP, std::string("dcol_prox_pair: ") + hipGetErrorString(q));
-            }
-        }
-        if (!seen) return fail(DCOL_ERR_HIP, "dcol_prox_pair: the launch ended without its completion flag");
-    } else {
-        const hipError_t e = hipStreamSynchronize(t->pair_stream);
-        if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_prox_pair: ") + hipGetErrorString(e));
-    }
+    const hipError_t e = hipStreamSynchronize(t->pair_stream);
+    if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_prox_pair: ") + hipGetErrorString(e));
     *alpha = h->alpha;
     if (contact && (flags & DCOL_CONTACT)) std::memcpy(contact, h->contact, 3 * sizeof(double));
     if (grad && (flags & DCOL_GRAD_ANY)) std::memcpy(grad, h->grad, 12 * sizeof(double));

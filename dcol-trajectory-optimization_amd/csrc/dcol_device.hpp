@@ -181,12 +181,6 @@ struct KArgs {
     int32_t* susp_pi;                   // [susp_cap] pair index (slot index into perm space)
     double* susp_state;                 // [fields][susp_cap]: it, x[N], then (s, z, r) per lane row
     int64_t susp_cap;
-    // One-pair launches of dcol_prox_pair (a single workgroup): after every output store of
-    // the launch, thread 0 stores done_seq to *done -- device-mapped pinned host memory,
-    // system-scope release -- so the caller polls host memory for completion instead of
-    // synchronising the stream.  nullptr: none.
-    int32_t* done = nullptr;
-    int32_t done_seq = 0;
 #ifdef DCOL_STAMPS
     unsigned long long* stamps;         // diagnostic build only (tools/stamp_probe.hip): [B][16]
 #endif
@@ -2177,14 +2171,6 @@ __global__ void __launch_bounds__(kSolveBlock, WPS) prox_kernel(KArgs A) {
     if (slot >= A.n) return;
     const int64_t pi = A.perm ? (int64_t)A.perm[A.slot0 + slot] : (A.slot0 + slot);
     solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0, OE, (FL & 16) ? 1 : 0>(A, pi, q);
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(DCOL_NO_DONE_FLAG)
-    // the pair's lanes are in this wave and reconverged here: the fence waits for all of the
-    // wave's stores (the other lanes' gradient entries included) before the flag is released
-    if (A.done && t == 0) {
-        __threadfence_system();
-        __hip_atomic_store(A.done, A.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-#endif
 }
 
 // The resume launch of a suspend / resume pair: one lane group per continuation entry;

@@ -55,8 +55,7 @@ struct PairBox {
     int32_t flags, max_iter;
     uint64_t req;   // seq << 32 | lpp << 16 | vid
     uint64_t ids;   // (seq & 0xffff) << 48 | s2 << 24 | s1   (shape ids below 2^24)
-    int32_t done, alive, stop;
-    int32_t launch_done;   // completion flag of a one-pair launch outside the server (KArgs::done)
+    int32_t done, alive, stop, pad_;
     int64_t solve_ticks, solve_cycles;   // the last served request: wall-clock ticks and shader cycles
 };
 constexpr int kPairBoxIdBits = 24;

@@ -2,6 +2,7 @@
 """Where the drop-in's per-call latency goes (bench.py `dropin`): one quadrotor pair kind at
 a time, timed on the host clock over many calls --
   python   : proximity_mrp / proximity_gradient (the drop-in, Python + C + GPU)
+  device   : of those, the one-pair server's request-to-answer time on the device
   batch_host: the same pair through solve_objects -> dcol_prox_batch_host (round 2's path)
   c_call   : dcol_prox_pair through ctypes with pre-built arguments (C + GPU)
   plan_run : the same one-pair plan on device-resident poses, launch + hipStreamSynchronize
@@ -56,8 +57,15 @@ def main():
     for o in obs:
         kind = type(o).__name__
         row = {"obstacle": kind}
+        s0 = eng.pair_stats()
         row["python_mrp_us"] = best_us(lambda: proximity_mrp(vic, o), args.calls)
+        s1 = eng.pair_stats()
         row["python_grad_us"] = best_us(lambda: proximity_gradient(vic, o), args.calls)
+        s2 = eng.pair_stats()
+        for key, a, b in (("device_mrp_us", s0, s1), ("device_grad_us", s1, s2)):
+            n = b["served"] - a["served"]   # one-pair server: request-to-answer time on the device
+            if n > 0:
+                row[key] = (b["server_solve_us"] - a["server_solve_us"]) / n
         # round 2's per-call path: a transient plan + pageable staging (dcol_prox_batch_host)
         row["batch_host_grad_us"] = best_us(lambda: eng.solve_objects([vic], [o], grad="fd", contact=False), args.calls)
         s1, s2 = eng.register_object(vic), eng.register_object(o)
