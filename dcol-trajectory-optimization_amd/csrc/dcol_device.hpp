@@ -1985,8 +1985,7 @@ DCOL_HD void launder(P& p) {
 // the launch is a ball block (Solver).  The host picks the variant per launch
 // (dcol_capi.cpp: bucket_pairs).
 // MODE 0: one launch; 1: main launch of a suspend / resume pair (KArgs susp_*); 2: the
-// resume launch, for continuation entry ci (pi = its pair); 3: the one-pair server (as 0, the
-// poses kept in registers for the gradient instead of re-read)
+// resume launch, for continuation entry ci (pi = its pair)
 template <int N, int NSOC, int OMAX, int LPP, bool FULL = false, bool BALL = false, bool CONE = false, int OE = 0,
           int MODE = 0>
 DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1, int k1o = -1, int k2o = -1) {
@@ -2046,14 +2045,12 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1, int k
         KArgs L = A;   // laundered copies of the table pointers: no load CSE across the loop
         launder(L.shapes);
         launder(L.rows);
-        if constexpr (MODE != 3) {   // MODE 3 (one-pair server, one wave): the poses stay live
-            launder(L.pose1);        // -- they sit in mapped host memory, a PCIe round trip away
-            launder(L.pose2);
+        launder(L.pose1);
+        launder(L.pose2);
 #pragma unroll
-            for (int c = 0; c < 6; ++c) {
-                th1[c] = L.pose1[c * B + pi];
-                th2[c] = L.pose2[c * B + pi];
-            }
+        for (int c = 0; c < 6; ++c) {
+            th1[c] = L.pose1[c * B + pi];
+            th2[c] = L.pose2[c * B + pi];
         }
         const DevShape& T1 = L.shapes[k1];
         const DevShape& T2 = L.shapes[k2];

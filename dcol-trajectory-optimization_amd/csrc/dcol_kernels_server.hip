@@ -91,13 +91,13 @@ __global__ void __launch_bounds__(kSolveBlock, 1) prox_pair_server(KArgs Args, P
             switch (vid) {   // NOLINT (empty in development builds)
 #define DCOL_SCASE(ID, NN, NS, OM, LP, FL)                                                       \
     case ID:                                                                                     \
-        solve_one<NN, NS, OM, LP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0, 0, 3>(A, 0, q, -1, k1, k2); \
+        solve_one<NN, NS, OM, LP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0>(A, 0, q, -1, k1, k2); \
         break;
                 DCOL_FUSED_VARIANTS(DCOL_SCASE)
 #undef DCOL_SCASE
 #define DCOL_SPCASE(ID, NN, NS, OM, LP, FL, OEE)                                                 \
     case ID:                                                                                     \
-        solve_one<NN, NS, OM, LP, (FL & 1) != 0, (FL & 2) != 0, false, OEE, 3>(A, 0, q, -1, k1, k2); \
+        solve_one<NN, NS, OM, LP, (FL & 1) != 0, (FL & 2) != 0, false, OEE>(A, 0, q, -1, k1, k2); \
         break;
                 DCOL_FUSED_PART_VARIANTS(DCOL_SPCASE)
 #undef DCOL_SPCASE

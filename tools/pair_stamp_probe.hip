@@ -45,16 +45,18 @@ void probe(const char* name, const Dev& d, int reps) {
         a.shapes = d.sh; a.rows = d.rw; a.s1 = d.s1; a.s2 = d.s2; a.pose1 = d.p1; a.pose2 = d.p2;
         a.B = 1; a.slot0 = 0; a.n = 1; a.tol = 1e-6; a.max_iter = 50; a.flags = flags;
         a.alpha = d.al; a.contact = d.ct; a.grad = d.gr; a.iters = d.it; a.status = d.st; a.stamps = d.stamp;
-        std::vector<std::vector<double>> ph(6);
+        std::vector<std::vector<double>> ph(6), sub(7);
         int iters = 0, status = 0;
         for (int r = 0; r < reps; ++r) {
-            CK(hipMemset(d.stamp, 0, 128));
+            CK(hipMemset(d.stamp, 0, 128));   // (16 stamps: phases 0-5, iteration-2 sub-phases 8-15)
             hipLaunchKernelGGL((prox_kernel<N, NS, OM, LP, WP, FL>), dim3(1), dim3(kSolveBlock), 0, 0, a);
             CK(hipDeviceSynchronize());
             unsigned long long s[16];
             CK(hipMemcpy(s, d.stamp, 128, hipMemcpyDeviceToHost));
             for (int k = 0; k < 5; ++k) ph[k].push_back((double)(s[k + 1] - s[k]));
             ph[5].push_back((double)(s[5] - s[0]));
+            if (s[8] && s[15])
+                for (int k = 0; k < 7; ++k) sub[k].push_back((double)(s[9 + k] - s[8 + k]));
             CK(hipMemcpy(&iters, d.it, 4, hipMemcpyDeviceToHost));
             CK(hipMemcpy(&status, d.st, 4, hipMemcpyDeviceToHost));
         }
@@ -63,6 +65,12 @@ void probe(const char* name, const Dev& d, int reps) {
         for (int k = 0; k < 6; ++k) {
             std::sort(ph[k].begin(), ph[k].end());
             std::printf("    %-14s %8.0f cyc\n", k < 5 ? names[k] : "total", ph[k][ph[k].size() / 2]);
+        }
+        const char* subn[7] = {"NT + normal matrix", "Cholesky", "predictor + bound", "rho, sigma, cp",
+                               "corrector rhs", "corrector bound", "update"};
+        for (int k = 0; k < 7 && !sub[k].empty(); ++k) {
+            std::sort(sub[k].begin(), sub[k].end());
+            std::printf("      it2 %-18s %6.0f cyc\n", subn[k], sub[k][sub[k].size() / 2]);
         }
     }
 }
