@@ -903,7 +903,10 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
     if (!t->pair_host) {
         hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&t->pair_host), sizeof(PairBox),
                                      hipHostMallocMapped | hipHostMallocPortable);
-        if (e == hipSuccess) std::memset(t->pair_host, 0, sizeof(PairBox));   // flags and sequence numbers start at 0
+        if (e == hipSuccess) {
+            std::memset(t->pair_host, 0, sizeof(PairBox));   // flags and sequence numbers start at 0
+            t->pair_host->xcd = -1;                           // no server yet
+        }
         if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&t->pair_dev), t->pair_host, 0);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&t->pair_stream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&t->server_stream, hipStreamNonBlocking);
@@ -1075,7 +1078,7 @@ int dcol_table_pair_plans(const dcol_table* tc, int32_t* n) {
 }
 
 int dcol_table_pair_stats(const dcol_table* tc, int64_t* served, int64_t* launched, int64_t* server_starts,
-                          double* server_solve_us, double* server_solve_cycles) {
+                          double* server_solve_us, double* server_solve_cycles, int32_t* server_xcd) {
     if (!tc) return fail(DCOL_ERR_ARG, "dcol_table_pair_stats: NULL table");
     dcol_table* t = const_cast<dcol_table*>(tc);
     std::lock_guard<std::mutex> lk(t->mu);
@@ -1084,6 +1087,7 @@ int dcol_table_pair_stats(const dcol_table* tc, int64_t* served, int64_t* launch
     if (server_starts) *server_starts = t->n_starts;
     if (server_solve_us) *server_solve_us = t->srv_us;
     if (server_solve_cycles) *server_solve_cycles = t->srv_cycles;
+    if (server_xcd) *server_xcd = t->pair_host ? __atomic_load_n(&t->pair_host->xcd, __ATOMIC_ACQUIRE) : -1;
     return DCOL_SUCCESS;
 }
 

@@ -50,6 +50,7 @@ __global__ void __launch_bounds__(kSolveBlock, 1) prox_pair_server(KArgs Args, P
     constexpr uint64_t kIdMask = (1ull << kPairBoxIdBits) - 1;
     int32_t last = box_ld(&box->done);
     box_st(&box->alive, 1);
+    box_st(&box->xcd, __builtin_amdgcn_s_getreg(6164) & 0xf);   // hwreg(HW_REG_XCC_ID, 0, 4)
     long long t0 = wall_clock64();
     for (;;) {
         // one round trip per poll: the id word and the stop flag in flight with the request word

@@ -55,7 +55,8 @@ struct PairBox {
     int32_t flags, max_iter;
     uint64_t req;   // seq << 32 | lpp << 16 | vid
     uint64_t ids;   // (seq & 0xffff) << 48 | s2 << 24 | s1   (shape ids below 2^24)
-    int32_t done, alive, stop, pad_;
+    int32_t done, alive, stop;
+    int32_t xcd;   // the XCD the running server sits on (HW_REG_XCC_ID; dcol_table_pair_stats)
     int64_t solve_ticks, solve_cycles;   // the last served request: wall-clock ticks and shader cycles
 };
 constexpr int kPairBoxIdBits = 24;

@@ -63,7 +63,7 @@ SIGNATURES = {
                                c_void_p, c_void_p, c_void_p, c_void_p]),
     "dcol_table_pair_plans": (c_int, [c_void_p, POINTER(c_int32)]),
     "dcol_table_pair_stats": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64),
-                                      POINTER(c_double), POINTER(c_double)]),
+                                      POINTER(c_double), POINTER(c_double), POINTER(c_int32)]),
     "dcol_comm_unique_id": (c_int, [c_void_p]),
     "dcol_comm_create": (c_int, [c_void_p, c_int32, c_int32, c_int32, POINTER(c_void_p)]),
     "dcol_comm_destroy": (c_int, [c_void_p]),

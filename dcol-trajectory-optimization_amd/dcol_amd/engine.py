@@ -384,12 +384,12 @@ class Engine:
         """dcol_table_pair_stats of the current table: {"served": calls the one-pair server
         answered, "launched": calls that launched their own kernel, "server_starts",
         "server_solve_us" / "server_solve_cycles": device time from request to answer summed
-        over the served calls}."""
+        over the served calls, "server_xcd": the XCD the last server started on}."""
         with self._lock:
-            v = [ctypes.c_int64() for _ in range(3)] + [ctypes.c_double() for _ in range(2)]
+            v = [ctypes.c_int64() for _ in range(3)] + [ctypes.c_double() for _ in range(2)] + [ctypes.c_int32()]
             _lib.check(_lib.load().dcol_table_pair_stats(self.table.handle, *[ctypes.byref(x) for x in v]),
                        "dcol_table_pair_stats")
-            keys = ("served", "launched", "server_starts", "server_solve_us", "server_solve_cycles")
+            keys = ("served", "launched", "server_starts", "server_solve_us", "server_solve_cycles", "server_xcd")
             return {k: x.value for k, x in zip(keys, v)}
 
 

@@ -208,11 +208,13 @@ int dcol_prox_pair(const dcol_table* table, int32_t shape1, int32_t shape2, cons
 #define DCOL_PAIR_PLANS_MAX 64
 int dcol_table_pair_plans(const dcol_table* table, int32_t* n);
 /* Counters of dcol_prox_pair on this table: calls answered by the server, calls that
- * launched their own kernel, server starts, and over the served calls the device time from
- * the server seeing a request to its answer: microseconds and shader-clock cycles (sums;
- * their ratio is the clock the solves ran at).  Any pointer may be NULL.                 */
+ * launched their own kernel, server starts, over the served calls the device time from the
+ * server seeing a request to its answer (microseconds and shader-clock cycles, sums: their
+ * ratio is the clock the solves ran at), and the XCD (0-7) the last server started on (-1:
+ * none yet).  Any pointer may be NULL.                                                   */
 int dcol_table_pair_stats(const dcol_table* table, int64_t* served, int64_t* launched,
-                          int64_t* server_starts, double* server_solve_us, double* server_solve_cycles);
+                          int64_t* server_starts, double* server_solve_us, double* server_solve_cycles,
+                          int32_t* server_xcd);
 
 /* ---- multi-GPU ------------------------------------------------------
  * One process per GPU.  Pairs are independent, so each rank solves its own shard with its

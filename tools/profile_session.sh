@@ -10,10 +10,11 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 B="python3 bench.py --no-cpu --no-altro --check 0 --steps 200 --warmup 100 --streams 1 --mixed-steps 0 --no-kernel-1m"
 M="python3 bench.py --workload mixed1m --no-cpu --no-altro --check 0 --steps 20 --warmup 5"
-tools/gpu_session.sh \
+OUT=$OUT tools/gpu_session.sh \
   "tests|600|python3 -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread" \
   "smoke|120|python3 -c 'import __graft_entry__ as g; g.smoke()'" \
   "bench_default|400|python3 bench.py" \
+  "bench_driver|400|python3 bench.py --gpus 1 --steps 20 --warmup 5" \
   "trace|300|rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- $B" \
   "trace_mixed|300|rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace_mixed -o run -- $M" \
   "pmc_fetch|300|rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/pmc_fetch -o run -- $B" \
