@@ -403,7 +403,7 @@ def kernel_1m(args, eng, ids, tab, dev, reps=20):
     """The solve kernel's steady state, apart from the 100k launch's quantisation (3,125 waves
     over 2,048 wave slots: 1.53 rounds, the last one partly empty): ONE launch of 1M pairs of
     the same distribution (15.3 rounds), kernel only, HIP events on the launch stream (median
-    of `reps` after 10 warm-up launches), with its FP64 roofline fraction (counted flops)."""
+    of `reps` after 40 warm-up launches), with its FP64 roofline fraction (counted flops)."""
     import torch
     from dcol_amd import alloc_outputs
     B = 1_000_000
@@ -414,7 +414,7 @@ def kernel_1m(args, eng, ids, tab, dev, reps=20):
     out = alloc_outputs(B, dev, want_grad=True, want_contact=False)
     stream = torch.cuda.current_stream(dev)
     run = plan.bind(d1, d2, out, grad=args.grad, contact=False, stream=stream)
-    for _ in range(10):
+    for _ in range(40):   # ~16 ms of launches: the clocks settle (profiles/r04_clock/)
         run()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     for e0, e1 in ev:
