@@ -164,7 +164,7 @@ PART = {
     # x sphere / cone: both lanes own a SOC block (capsule x sphere 11.2e8 at LPP 2, 9.1e8 at 1)
     # two waves per SIMD where the allocator then spills at most a few scratch accesses per
     # iteration (tools/isa_stats.py --waves 2) -- measured 200k pairs per class
-    # (profiles/r04_wps/): capsule x cone 7.82e8 -> 8.68e8, cone x capsule 7.92 -> 8.94e8
+    # (profiles/r04_base/cls_w*.log): capsule x cone 7.82e8 -> 8.68e8, cone x capsule 7.92 -> 8.94e8
     # ((4, 2), 2 scratch accesses per iteration), cylinder x cone 6.88 -> 7.35e8, cone x
     # cylinder 6.78 -> 7.35e8 ((6, 2), 21)
     (5, 2): {(2, 2): [(2, 1), (1, 1)], (4, 2): [(2, 2), (1, 1)], (6, 2): [(2, 2)]},
