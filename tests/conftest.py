@@ -70,10 +70,11 @@ def engine():
 
 
 def _ensure_built():
-    """Build lib/libdcol.so and lib/libdcol_altro.so in-tree if a fresh checkout lacks them
-    (hipcc cross-compiles for gfx950 without a GPU)."""
+    """Build lib/libdcol.so, lib/libdcol_altro.so and dcol_amd/_fastpair.so in-tree if a fresh
+    checkout lacks them (hipcc cross-compiles for gfx950 without a GPU)."""
     import subprocess
     libs = [os.path.join(PKG, "lib", n) for n in ("libdcol.so", "libdcol_altro.so")]
+    libs.append(os.path.join(PKG, "dcol_amd", "_fastpair.so"))
     if not all(os.path.exists(p) for p in libs):
         subprocess.run(["make", "-C", os.path.join(PKG, "csrc"), "-j8", "-s"], check=True)
 
