@@ -292,3 +292,43 @@ def test_pair_server_idle_exit_and_restart(engine, monkeypatch):
     s1 = engine.pair_stats()
     assert s1["served"] - s0["served"] == 40
     assert s1["server_starts"] - s0["server_starts"] >= 40   # every flag change restarts it
+
+
+@pytest.mark.gpu
+def test_pair_server_two_threads(engine):
+    """Two threads calling the drop-in on one engine (the fast path takes no Python lock: the
+    library serialises the calls per table): every answer bitwise equal to the same call made
+    alone, and equal to the reference's golden values."""
+    import copy
+    import threading
+    d = load_golden(GOLDEN["scene_quad"])
+    ok = np.flatnonzero(d["status"] == 0)
+    tol = float(d["tol"])
+    sets = []
+    for part in (ok[0::2][:40], ok[1::2][:40]):
+        objs = objects_from_golden(d)
+        sets.append([copy.deepcopy(pose_pair(objs, d, i)) + (i,) for i in part])
+    ref = {}
+    for s in sets:
+        for a, b, i in s:
+            ref[i] = engine.solve_pair(a, b, tol, grad="fd", contact=False)
+    got, errors = {}, []
+
+    def worker(s):
+        try:
+            for _ in range(3):
+                for a, b, i in s:
+                    got.setdefault(i, []).append(engine.solve_pair(a, b, tol, grad="fd", contact=False))
+        except BaseException as e:   # reported by the main thread
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=worker, args=(s,)) for s in sets]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors, errors
+    for i, rs in got.items():
+        for r in rs:
+            np.testing.assert_array_equal(_bits([r]), _bits([ref[i]]))
+        assert alpha_close(rs[0][0], d["alpha"][i]) and grad_close(rs[0][2], d["grad"][i])
