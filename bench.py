@@ -7,10 +7,13 @@ per GPU, B = 100,000 (knot x primitive-pair) problems; primitives are rect-prism
 pair); poses r ~ U(-3, 3)^3, p (MRP) ~ U(-1, 1)^3; seed 0 (+ rank).  One "step" = one
 dcol_plan_run over the whole batch: conic assembly + PDIP (pdip_tol 1e-6) + the 12-gradient
 (FD mode = the reference's formulation) + alpha, with poses already resident in HBM.
-Steps are issued round-robin on --streams (default 2) HIP streams, each with its own output
-buffers, as a pipelined batch service would: the last, partly-filled round of one step's
-waves overlaps the first round of the next.  The one-stream (serialised) throughput is
-reported beside it (pipeline.serial_value), and kernel_ms is the per-launch duration.
+`value` / `ms_per_step` are the one-stream run: K steps issued back to back on one HIP
+stream, each bracketed by HIP events on that stream, so `kernel_ms` (the mean of those
+event intervals) and the rooflines come from the same run and ms_per_step >= kernel_ms.
+Beside it, `pipeline`: the same steps issued round-robin on --streams (default 2) streams
+with their own output buffers, as a pipelined batch service would (the last, partly-filled
+round of one step's waves overlaps the first round of the next) -- an overlap rate, never
+`value`.
 
 Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE set) this process is one rank;
 `python bench.py --gpus N` without torchrun starts the N ranks itself (torch.distributed.run
@@ -199,6 +202,10 @@ def main():
                     help="GPU_MAX_HW_QUEUES for this process (HIP hardware queues; 0 = leave the environment's)")
     ap.add_argument("--no-kernel-1m", dest="kernel_1m", action="store_false",
                     help="skip the 1M-pair kernel-only steady-state section (kernel_1m)")
+    ap.add_argument("--deadline-s", type=float, default=float(os.environ.get("DCOL_BENCH_DEADLINE_S", "180")),
+                    help="N > 1: the longest any rank waits for one phase (communicator set-up, a step's solve, its "
+                         "all-gather, a barrier) before it prints a JSON diagnostic (rank, step, phase) to stderr and "
+                         "exits non-zero (dcol_amd.dist.StepWatchdog)")
     ap.add_argument("--pack-pass", action="store_true",
                     help="mixed1m: per-pair arrays + pack_records kernel + out-of-place all-gather instead of "
                          "records written by the solver kernels with the all-gather in place (A/B)")
@@ -228,13 +235,20 @@ def main():
     if world > 1 and args.backend == "nccl" and ndev < world:
         print(f"bench.py: {world} RCCL ranks need {world} GPUs, this node shows {ndev}", file=sys.stderr)
         sys.exit(2)
+    wd = None
     if world > 1:
+        import datetime
+
         import torch.distributed as dist
+        from dcol_amd.dist import StepWatchdog
+        wd = StepWatchdog(rank, world, args.deadline_s)
         torch.cuda.set_device(local)
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(args.backend)
+        with guard(wd, "init_process_group"):
+            tmo = datetime.timedelta(seconds=args.deadline_s)
+            if args.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
+            else:
+                dist.init_process_group(args.backend, timeout=tmo)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local)
@@ -243,7 +257,7 @@ def main():
         print(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}", file=sys.stderr)
         sys.exit(2)
     if args.workload == "mixed1m":
-        return run_mixed(args, world, rank, local, dev, coll_dev, dist)
+        return run_mixed(args, world, rank, local, dev, coll_dev, dist, wd)
 
     from dcol_amd import Engine, spec_from_arrays
     tab = shape_table()
@@ -261,48 +275,63 @@ def main():
     step = plan.bind(pose1, pose2, out, grad=args.grad, contact=False, stream=stream, max_iter=args.max_iter)
     # pipelined issue: S streams, each with its own outputs (poses are read-only, shared)
     S = max(1, args.streams)
+    lane_streams = [stream] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     lanes = [step] + [plan.bind(pose1, pose2, alloc_outputs(B, dev, want_grad=True, want_contact=False),
-                                grad=args.grad, contact=False, stream=torch.cuda.Stream(dev), max_iter=args.max_iter)
-                      for _ in range(S - 1)]
+                                grad=args.grad, contact=False, stream=st, max_iter=args.max_iter)
+                      for st in lane_streams[1:]]
 
     for k in range(args.warmup):
-        lanes[k % S]()
-    torch.cuda.synchronize(dev)
+        step()
+    sync(dev, wd, "warmup")
 
-    def timed(fns):
-        """exactly K steps, barrier + synchronize on both sides, no events"""
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for k in range(args.steps):
-            fns[k % len(fns)]()
-        torch.cuda.synchronize(dev)
-        if dist is not None:
-            dist.barrier()
-        return time.perf_counter() - t0
-
-    elapsed_serial = timed([step]) if S > 1 else None
-    elapsed = timed(lanes)
-
-    # kernel duration (roofline): HIP events on the launch stream, separate pass
+    # value: exactly K steps on ONE stream, barrier + synchronize on both sides; each step
+    # bracketed by HIP events on that stream (the kernel duration of this same run)
+    barrier(dist, wd, "barrier before the timed steps")
+    sync(dev, wd, "synchronize before the timed steps")
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
     for k in range(args.steps):
         ev[k][0].record(stream)
         step()
         ev[k][1].record(stream)
-    torch.cuda.synchronize(dev)
+    for k in range(args.steps):       # (a rank that hangs names its step)
+        wait_event(ev[k][1], wd, "solve", k)
+    sync(dev, wd, "synchronize after the timed steps")
+    elapsed = time.perf_counter() - t0
+    barrier(dist, wd, "barrier after the timed steps")
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    # pipeline: the same K steps round-robin on S streams (an overlap rate, reported beside)
+    elapsed_pipe = None
+    if S > 1:
+        for k in range(args.warmup):
+            lanes[k % S]()
+        sync(dev, wd, "pipeline warmup")
+        barrier(dist, wd, "barrier before the pipelined steps")
+        sync(dev, wd, "synchronize before the pipelined steps")
+        t0 = time.perf_counter()
+        done = []
+        for k in range(args.steps):
+            lanes[k % S]()
+            e = torch.cuda.Event()
+            e.record(lane_streams[k % S])
+            done.append(e)
+        for k, e in enumerate(done):
+            wait_event(e, wd, "pipelined solve", k)
+        sync(dev, wd, "synchronize after the pipelined steps")
+        elapsed_pipe = time.perf_counter() - t0
+        barrier(dist, wd, "barrier after the pipelined steps")
     # (kernel_1m right after the timed steps, while the clocks are still at their loaded level:
     # after end_to_end's host-side staging the GPU has idled and re-ramps through the first
     # ~10 ms of launches -- measured 0.44 ms per 1M launch there against 0.36 ms)
     k1m = kernel_1m(args, eng, ids, tab, dev) if world == 1 and args.kernel_1m else None
     e2e = end_to_end(args, eng, ids, s1, s2, p1, p2, pose1, pose2, out, step, dev) if world == 1 else None
     if dist is not None:
-        t = torch.tensor([elapsed, kern_ms, elapsed_serial or 0.0], device=coll_dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t = torch.tensor([elapsed, kern_ms, elapsed_pipe or 0.0], device=coll_dev, dtype=torch.float64)
+        with guard(wd, "all_reduce of the timings"):
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms_max = float(t[0]), float(t[1])
-        elapsed_serial = float(t[2]) if elapsed_serial is not None else None
+        elapsed_pipe = float(t[2]) if elapsed_pipe is not None else None
     else:
         kern_ms_max = kern_ms
 
@@ -311,11 +340,14 @@ def main():
     alpha = out["alpha"].cpu().numpy()
     grad = out["grad"].cpu().numpy()
     # configs[4] on the same ranks (every rank takes part: one all-gather per step)
-    mixed = (mixed_measure(args, world, rank, local, dev, coll_dev, dist, args.mixed_steps, min(args.warmup, 5))
+    mixed = (mixed_measure(args, world, rank, local, dev, coll_dev, dist, args.mixed_steps, min(args.warmup, 5), wd)
              if args.mixed_steps > 0 else None)
 
     if rank != 0:
-        dist.destroy_process_group()
+        with guard(wd, "destroy_process_group"):
+            dist.destroy_process_group()
+        if wd is not None:
+            wd.close()
         return
 
     total = B * world * args.steps
@@ -331,6 +363,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": 1e3 * elapsed / args.steps,
+        "kernel_ms": kern_ms,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -348,12 +381,13 @@ def main():
                           "flops_per_pair": flops_pair,
                           "flops_source": "op-counting C restatement, profiles/flop_model.json"
                           if os.path.exists(os.path.join(REPO, "profiles", "flop_model.json")) else "hand model"},
-        "pipeline": {"streams": S, "note": "steps issued round-robin on S streams with separate outputs; "
-                     "value/ms_per_step are the pipelined throughput, serial_* the one-stream run",
+        "timing": "value = pairs / ms_per_step of K steps on one stream; kernel_ms = the mean HIP-event duration "
+                  "of those same K launches (events on the launch stream), the rooflines' time base",
+        "pipeline": {"streams": S, "note": "the same K steps issued round-robin on S streams with separate outputs "
+                     "(an overlap rate: one step's last round of waves overlaps the next step's first; not value)",
                      "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
-                     "serial_value": (B * world * args.steps / elapsed_serial) if elapsed_serial else value,
-                     "serial_ms_per_step": 1e3 * (elapsed_serial or elapsed) / args.steps},
-        "kernel_ms": kern_ms,
+                     "value": (B * world * args.steps / elapsed_pipe) if elapsed_pipe else None,
+                     "ms_per_step": 1e3 * elapsed_pipe / args.steps if elapsed_pipe else None},
         "kernel_ms_max_rank": kern_ms_max,
         "world": {"ranks": world, "process_group_size": dist.get_world_size() if dist is not None else 1,
                   "backend": args.backend if dist is not None else None, "devices_visible": ndev},
@@ -394,9 +428,65 @@ def main():
         line["cpu_baseline_c"] = cpu_baseline_c(tab, s1, s2, p1, p2, workers)
         for k in ("cpu_baseline", "cpu_baseline_c"):
             line[k]["host_cpus"] = host
+    line["summary"] = summary(line)    # last: the part of the line a truncated tail still shows
     print(json.dumps(line), flush=True)
     if dist is not None:
-        dist.destroy_process_group()
+        with guard(wd, "destroy_process_group"):
+            dist.destroy_process_group()
+        wd.close()
+
+
+def summary(line):
+    """The headline figures of every section in one short object (printed last)"""
+    m = line.get("mixed1m") or {}
+    d = line.get("dropin") or {}
+    out = {"value": line["value"], "ms_per_step": line["ms_per_step"], "kernel_ms": line["kernel_ms"],
+           "fp64_frac": line["roofline_fp64"]["frac"], "hbm_frac": line["roofline"]["frac"],
+           "pipelined_value": line["pipeline"]["value"]}
+    if m:
+        out["mixed1m"] = {"value": m["value"], "ms_per_step": m["ms_per_step"], "kernel_ms": m.get("kernel_ms"),
+                          "fp64_frac": (m.get("roofline_fp64") or {}).get("frac"),
+                          "pipelined_value": m["pipeline"]["value"]}
+    if "kernel_1m" in line:
+        out["kernel_1m"] = {"pair_solves_per_s": line["kernel_1m"]["pair_solves_per_s"],
+                            "fp64_frac": line["kernel_1m"]["roofline_fp64"]["frac"]}
+    if d:
+        out["dropin_us_per_call"] = {k: d[k]["us_per_call"] for k in ("proximity_mrp", "proximity_gradient") if k in d}
+    if "altro" in line:
+        out["altro_ms_per_iter"] = {k: v["ms_per_iter"] for k, v in line["altro"]["systems"].items()}
+    if "cpu_baseline" in line:
+        out["cpu_baseline"] = line["cpu_baseline"]["value"]
+    return out
+
+
+def guard(wd, phase, step=None):
+    """the rank's deadline around one wait (N > 1); no-op without a watchdog"""
+    import contextlib
+    return wd.guard(phase, step) if wd is not None else contextlib.nullcontext()
+
+
+def sync(dev, wd, phase):
+    """torch.cuda.synchronize under the rank's deadline (N > 1)"""
+    import torch
+    if wd is None:
+        torch.cuda.synchronize(dev)
+        return
+    with guard(wd, phase):   # (torch.cuda.synchronize releases the GIL while it waits)
+        torch.cuda.synchronize(dev)
+
+
+def barrier(dist, wd, phase):
+    if dist is None:
+        return
+    with guard(wd, phase):
+        dist.barrier()
+
+
+def wait_event(e, wd, phase, step):
+    if wd is None:
+        e.synchronize()
+    else:
+        wd.wait_event(e, phase, step)
 
 
 def kernel_1m(args, eng, ids, tab, dev, reps=20):
@@ -539,22 +629,24 @@ def mixed_pairs(tab, B, seed):
     return s1, s2, pose1, pose2
 
 
-def run_mixed(args, world, rank, local, dev, coll_dev, dist):
+def run_mixed(args, world, rank, local, dev, coll_dev, dist, wd=None):
     """--workload mixed1m: BASELINE configs[4] as the bench line itself (strong scaling)."""
-    line = mixed_measure(args, world, rank, local, dev, coll_dev, dist, args.steps, args.warmup)
+    line = mixed_measure(args, world, rank, local, dev, coll_dev, dist, args.steps, args.warmup, wd)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
-        dist.destroy_process_group()
+        with guard(wd, "destroy_process_group"):
+            dist.destroy_process_group()
+        wd.close()
 
 
-def native_comm(NativeComm, dist, world, rank, local):
+def native_comm(NativeComm, dist, world, rank, local, wd=None):
     """(communicator, error) for the C-ABI RCCL path.  Rank 0 makes the unique id and ALWAYS
     takes part in its broadcast (None when it could not make one), so a failure on rank 0
     never leaves the other ranks in a collective rank 0 skipped; the ranks then all create
     the communicator or all skip it.  (A failure inside ncclCommInitRank itself cannot be
-    signalled to the ranks already waiting in it; the usual failure -- librccl not
-    loadable -- surfaces in the id step.)"""
+    signalled to the ranks already waiting in it: the rank's deadline (wd) ends that wait;
+    the usual failure -- librccl not loadable -- surfaces in the id step.)"""
     uid, err = [None], None
     if rank == 0:
         try:
@@ -562,25 +654,32 @@ def native_comm(NativeComm, dist, world, rank, local):
         except Exception as e:
             err = f"{type(e).__name__}: {e}"
     if dist is not None:
-        dist.broadcast_object_list(uid, src=0)
+        with guard(wd, "communicator id broadcast"):
+            dist.broadcast_object_list(uid, src=0)
     if uid[0] is None:
         return None, err or "rank 0 could not create a communicator id"
     try:
-        return NativeComm(uid[0], world, rank, local), None
+        with guard(wd, "communicator set-up (ncclCommInitRank)"):
+            return NativeComm(uid[0], world, rank, local), None
     except Exception as e:   # recorded in the line; the step then uses torch.distributed
         return None, f"{type(e).__name__}: {e}"
 
 
-def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
+def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup, wd=None):
     """BASELINE configs[4]: 1M mixed-primitive pairs sharded over the ranks (class-balanced
     round-robin, dcol_amd.dist.shard_indices), each shard solved on its GPU from
     HBM-resident poses, then ONE all-gather of the packed per-pair record [alpha, grad(12),
-    status, iters] so every rank holds the whole batch.  The timed step = solve + pack +
+    status, iters] so every rank holds the whole batch.  The timed step = solve + records +
     all-gather (strong scaling: the batch is fixed as N grows).  With the RCCL backend the
-    step is the shipped C-ABI path: dcol_prox_batch_multi_gpu (plan run -> pack_records
-    kernel -> ncclAllGather on the launch stream, communicator from dcol_comm_create);
-    gloo rehearsals (several ranks on one GPU, which RCCL refuses) and --torch-gather go
-    through torch.distributed.  Returns the line (rank 0) or None."""
+    step is the shipped C-ABI path: dcol_prox_batch_multi_gpu (the solver kernels write the
+    records into this rank's rows of the gathered buffer, DCOL_NO_GATHER) then
+    dcol_comm_all_gather (ncclAllGather in place), both on the launch stream; gloo rehearsals
+    (several ranks on one GPU, which RCCL refuses) and --torch-gather go through
+    torch.distributed.  value / ms_per_step: K such steps on ONE stream, each bracketed by
+    HIP events on it (start, solved, gathered), so kernel_ms -- the solve's share of each
+    step -- comes from the same run; the pipelined rate (solves round-robin on --streams
+    streams, all-gathers on one collective stream) is reported beside it.  With a deadline
+    (wd, N > 1) every wait names its phase and step.  Returns the line (rank 0) or None."""
     import torch
     from dcol_amd import Engine, alloc_outputs, spec_from_arrays
     from dcol_amd.dist import REC, NativeComm, shard_indices
@@ -603,33 +702,43 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
     comm, path = None, "torch.distributed all_gather_into_tensor" if dist is not None else "local copy (world 1)"
     native_error = None
     if args.backend == "nccl" and not args.torch_gather:
-        comm, native_error = native_comm(NativeComm, dist, world, rank, local)
+        comm, native_error = native_comm(NativeComm, dist, world, rank, local, wd)
         if dist is not None:     # every rank takes the same path
             ok = torch.tensor([0.0 if comm is None else 1.0], device=coll_dev)
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            with guard(wd, "communicator agreement (all_reduce)"):
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
             if ok.item() < 1.0 and comm is not None:
                 comm.close()
                 comm, native_error = None, native_error or "another rank could not create its communicator"
         if comm is not None:
             path = ("C-ABI dcol_prox_batch_multi_gpu (pack_records + ncclAllGather, RCCL)" if args.pack_pass else
                     "C-ABI dcol_prox_batch_multi_gpu in place (records written by the solver kernels into the "
-                    "gathered buffer, ncclAllGather in place, RCCL)")
+                    "gathered buffer, DCOL_NO_GATHER) + dcol_comm_all_gather (ncclAllGather in place, RCCL)")
     rec = torch.full((cap, REC), float("nan"), dtype=torch.float64, device=dev)
     gathered = torch.empty((world * cap, REC), dtype=torch.float64, device=dev if comm is not None else coll_dev)
+
+    # Each step function issues step k on its stream(s) and returns (stream, solved, gathered):
+    # events recorded after the step's solve and after its all-gather (None where the
+    # all-gather is host-synchronous: torch.distributed with gloo / world 1).
+    def ev():
+        return torch.cuda.Event(enable_timing=True)
 
     lanes = []
     if comm is not None and args.pack_pass:
         # the pack kernel + out-of-place all-gather (A/B): one stream, one communicator
-        def step():
+        def step(k):
+            e = ev()
             comm.solve_gather(plan, d1, d2, cap, grad=args.grad, out=out, stream=stream, rec_local=rec, rec_all=gathered)
+            e.record(stream)
+            return e, e
 
         def solve_only():   # its solve: the plan run with the per-pair arrays
             launch()
     elif comm is not None:
-        # records written by the solver kernels, all-gather in place.  Steps are issued
-        # round-robin on --streams solve streams, each with its own gathered buffer; every
-        # all-gather goes through the ONE communicator on ONE collective stream, in issue order
-        # on every rank: step k's solve (DCOL_NO_GATHER) -> event -> its all-gather on the
+        # records written by the solver kernels, all-gather in place.  The pipelined steps are
+        # issued round-robin on --streams solve streams, each with its own gathered buffer;
+        # every all-gather goes through the ONE communicator on ONE collective stream, in issue
+        # order on every rank: step k's solve (DCOL_NO_GATHER) -> event -> its all-gather on the
         # collective stream -> event that step k + S's solve waits for before it overwrites the
         # buffer.  So step k + 1's solve overlaps step k's all-gather (a batch service's steady
         # state) without two communicators or collectives on two streams.
@@ -637,26 +746,36 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
         nst = max(1, args.streams)
         bufs = [gathered] + [torch.empty((world * cap, REC), dtype=torch.float64, device=dev) for _ in range(nst - 1)]
         sstreams = [stream] + [torch.cuda.Stream(dev) for _ in range(nst - 1)]
-        solved = [torch.cuda.Event() for _ in range(nst)]
-        gdone = [torch.cuda.Event() for _ in range(nst)]
+        gdone = [None] * nst
 
         def lane_fn(j):
             st, g_ = sstreams[j], bufs[j]
 
-            def f():
-                st.wait_event(gdone[j])
+            def f(k):
+                if gdone[j] is not None:
+                    st.wait_event(gdone[j])
                 comm.solve_gather(plan, d1, d2, cap, grad=args.grad, stream=st, rec_all=g_, in_place=True, soa=False,
                                   gather=False)
-                solved[j].record(st)
-                cstream.wait_event(solved[j])
+                solved = ev()
+                solved.record(st)
+                cstream.wait_event(solved)
                 comm.all_gather(cap, g_, stream=cstream)
-                gdone[j].record(cstream)
+                gd = ev()
+                gd.record(cstream)
+                gdone[j] = gd
+                return solved, gd
             return f
         lanes = [lane_fn(j) for j in range(nst)]
 
-        def step():          # one step on the launch stream: solve, then the all-gather on it
+        def step(k):          # one step on the launch stream: the solve, then the all-gather on it
             comm.solve_gather(plan, d1, d2, cap, grad=args.grad, stream=stream, rec_all=gathered, in_place=True,
-                              soa=False)
+                              soa=False, gather=False)
+            solved = ev()
+            solved.record(stream)
+            comm.all_gather(cap, gathered, stream=stream)
+            gd = ev()
+            gd.record(stream)
+            return solved, gd
 
         def solve_only():    # the same solve and record writes without the all-gather (DCOL_NO_GATHER)
             comm.solve_gather(plan, d1, d2, cap, grad=args.grad, stream=stream, rec_all=gathered, in_place=True,
@@ -670,54 +789,74 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
             rec[:n, 13] = ((out["iters"].to(torch.int64) << 32) | (out["status"].to(torch.int64) & 0xFFFFFFFF)).view(
                 torch.float64)
 
-        def step():
+        def step(k):
             solve_only()
+            solved = ev()
+            solved.record(stream)
             if dist is not None:
-                dist.all_gather_into_tensor(gathered, rec.to(coll_dev))
+                src = rec.to(coll_dev)
+                with guard(wd, "all-gather", k):
+                    dist.all_gather_into_tensor(gathered, src)
             else:
                 gathered.copy_(rec)
+            gd = ev()
+            gd.record(stream)
+            return solved, gd
 
-    def timed(fns):
+    def settle(phase):
+        torch.cuda.synchronize(dev) if wd is None else sync(dev, wd, phase)
+
+    def run_steps(fns, phase):
+        """warm-up, then exactly `steps` steps timed between barrier + synchronize pairs;
+        (elapsed s max over ranks, per-step [start, solved, gathered] events)"""
         for k in range(warmup):
-            fns[k % len(fns)]()
-        torch.cuda.synchronize(dev)
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
+            fns[k % len(fns)](k)
+        settle(phase + " warmup")
+        barrier(dist, wd, "barrier before the " + phase + " steps")
+        settle("synchronize before the " + phase + " steps")
+        marks = []
         t0 = time.perf_counter()
         for k in range(steps):
-            fns[k % len(fns)]()
-        torch.cuda.synchronize(dev)
-        if dist is not None:
-            dist.barrier()
+            st = sstreams[k % len(fns)] if fns is lanes else stream
+            e0 = ev()
+            e0.record(st)
+            marks.append((e0,) + tuple(fns[k % len(fns)](k)))
+        for k, (_, solved, gd) in enumerate(marks):   # (a rank that hangs names its step and phase)
+            wait_event(solved, wd, phase + " solve", k)
+            wait_event(gd, wd, phase + " all-gather", k)
+        settle("synchronize after the " + phase + " steps")
         el = time.perf_counter() - t0
+        barrier(dist, wd, "barrier after the " + phase + " steps")
         if dist is not None:
             t = torch.tensor([el], device=coll_dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            with guard(wd, "all_reduce of the " + phase + " time"):
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t[0])
-        return el
+        return el, marks
 
-    elapsed_serial = timed([step]) if len(lanes) > 1 else None
-    elapsed = timed(lanes if len(lanes) > 1 else [step])
+    elapsed, marks = run_steps([step], "serial")
+    # the solve's share of each timed step (start -> solved) and the whole step, same run
+    kernel_ms = float(np.median([a.elapsed_time(b) for a, b, _ in marks]))
+    step_ev_ms = float(np.median([a.elapsed_time(c) for a, _, c in marks]))
+    elapsed_pipe = run_steps(lanes, "pipelined")[0] if len(lanes) > 1 else None
 
     def ev_times(fns, reps=20):
         """HIP-event durations [reps, len(fns)] (ms), the fns interleaved rep by rep (the same
         clock state for all of them)"""
-        ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in fns]
-              for _ in range(reps)]
-        for row in ev:
+        evs = [[(ev(), ev()) for _ in fns] for _ in range(reps)]
+        for row in evs:
             for fn, (e0, e1) in zip(fns, row):
                 e0.record(stream)
                 fn()
                 e1.record(stream)
-        torch.cuda.synchronize(dev)
-        return np.array([[e0.elapsed_time(e1) for e0, e1 in row] for row in ev])
+        settle("step breakdown")
+        return np.array([[e0.elapsed_time(e1) for e0, e1 in row] for row in evs])
     # like for like (HIP events on the launch stream, one step at a time, interleaved): solve =
     # the step's own solve and record writes without its collective; step = the same with it;
     # their difference is the communication cost of the step (SURVEY.md section 8e: 5-50 %
-    # predicted at 8 GPUs).  kernel = the plan run with the per-pair arrays (FP64 roofline).
-    tt = ev_times([solve_only, step, launch])
-    solve_ms, step_ms, kernel_ms = (float(v) for v in np.median(tt, axis=0))
+    # predicted at 8 GPUs).  plan = the plan run with the per-pair arrays.
+    tt = ev_times([solve_only, lambda: step(-1), launch])
+    solve_ms, step_ms, plan_ms = (float(v) for v in np.median(tt, axis=0))
     comm_d = tt[:, 1] - tt[:, 0]          # paired: each step against the solve just before it
     comm_ms = float(np.median(comm_d))
     comm_iqr = float(np.subtract(*np.percentile(comm_d, [75, 25])))
@@ -726,16 +865,17 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
     flops_local = mixed_flops(tab, s1[mine], s2[mine], my_iters, my_status, args.grad)
     # per-rank shard figures (load balance): solve ms, step ms, mean Newton iterations
     mine_stats = [solve_ms, step_ms, float(my_iters[my_status == 0].mean()) if (my_status == 0).any() else 0.0, float(n),
-                  kernel_ms]
+                  kernel_ms, plan_ms]
     if dist is not None:
-        t = torch.zeros((world, 5), device=coll_dev, dtype=torch.float64)
+        t = torch.zeros((world, len(mine_stats)), device=coll_dev, dtype=torch.float64)
         t[rank] = torch.tensor(mine_stats, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        with guard(wd, "all_reduce of the per-rank figures"):
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
         ranks_stats = t.cpu().numpy()
     else:
         ranks_stats = np.array([mine_stats])
     solve_ms_max = float(ranks_stats[:, 0].max())
-    torch.cuda.synchronize(dev)
+    settle("synchronize before the result copy")
     allrec = gathered.cpu().numpy().reshape(world, cap, REC)
     if comm is not None:
         comm.close()
@@ -750,6 +890,10 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
     line = {
         "metric": "PDIP proximity+grad pair-solves/sec", "value": B * steps / elapsed, "unit": "pair-solves/s",
         "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": 1e3 * elapsed / steps,
+        "kernel_ms": kernel_ms, "step_event_ms": step_ev_ms,
+        "timing": "value = pairs / ms_per_step of K steps on one stream (solve, then the all-gather, per step); "
+                  "kernel_ms = the median HIP-event time from a step's start to its solve's end, step_event_ms to "
+                  "its all-gather's end, in that same run (rank 0); the rooflines use kernel_ms",
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": "synthetic 1M mixed-primitive pairs sharded across GPUs + RCCL all-gather "
                                "(BASELINE.json configs[4])", "pairs_total": B, "pairs_per_gpu": cap,
@@ -771,12 +915,14 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
             "comm_ms_iqr_rank0": comm_iqr,
             "record_bytes_per_pair": REC * 8,
             "per_rank": {"solve_ms": ranks_stats[:, 0].tolist(), "step_ms": ranks_stats[:, 1].tolist(),
-                         "kernel_ms": ranks_stats[:, 4].tolist(),
+                         "kernel_ms": ranks_stats[:, 4].tolist(), "plan_run_ms": ranks_stats[:, 5].tolist(),
                          "iters_mean": ranks_stats[:, 2].tolist(), "pairs": ranks_stats[:, 3].astype(int).tolist()}},
-        "kernel_ms_rank0": kernel_ms,
+        "kernel_ms_max_rank": float(ranks_stats[:, 4].max()),
         "pipeline": {"streams": max(1, len(lanes)), "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
-                     "serial_value": B * steps / elapsed_serial if elapsed_serial else B * steps / elapsed,
-                     "serial_ms_per_step": 1e3 * (elapsed_serial or elapsed) / steps},
+                     "note": "solves round-robin on the streams, all-gathers on one collective stream (an overlap "
+                             "rate, not value)",
+                     "value": B * steps / elapsed_pipe if elapsed_pipe else None,
+                     "ms_per_step": 1e3 * elapsed_pipe / steps if elapsed_pipe else None},
     }
     if comm is not None:
         line["rccl_world_size"] = world
@@ -791,7 +937,7 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup):
                                  "unit": "TFLOP/s", "frac": tf / FP64_VECTOR_PEAK_TFS,
                                  "flops_per_pair": flops_local / max(n, 1),
                                  "note": "rank 0's shard: counted per-class flops (profiles/flop_model.json) at each "
-                                         "pair's iteration count / the shard's plan-run time (kernel_ms_rank0, HIP events)"}
+                                         "pair's iteration count / its solve time in the timed run (kernel_ms)"}
     if args.check:
         from oracle import c_oracle
         k = min(args.check * 8, B)

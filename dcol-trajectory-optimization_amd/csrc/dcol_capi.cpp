@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <chrono>
 #include <cstdio>
@@ -20,6 +21,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <unordered_map>
 #include <vector>
@@ -89,6 +91,20 @@ int pair_server_idle_us() {
     const long v = e ? std::atol(e) : 1000;
     return v < 0 ? 0 : (v > 1000000 ? 1000000 : (int)v);
 }
+// Tables of the process, so that dcol_shutdown can stop every resident pair server before
+// the process's HIP context and the servers' mapped mailboxes go away.  dcol_shutdown runs
+// from an exit handler registered at the first server start -- after the HIP runtime
+// initialised, so before its own exit-time teardown (exit handlers run last-registered
+// first) -- and from the Python binding's atexit hook (dcol_amd/_lib.py).  Lock order:
+// g_tables_mu, then a table's mu (dcol_prox_pair holds only the latter).
+std::mutex g_tables_mu;
+std::vector<dcol_table*> g_tables;
+std::atomic<bool> g_shutdown{false};   // set by dcol_shutdown: no new server starts
+std::once_flag g_exit_hook;
+// how long table destroy / shutdown / a restart wait for a server to leave (it leaves at its
+// next poll, i.e. after at most the solve in hand: microseconds)
+constexpr int kServerStopMs = 5000;
+
 bool device_side_streams(int dev, hipStream_t out[kSideStreams]) {
     DeviceSide& d = device_side(dev);
     std::lock_guard<std::mutex> lk(d.mu);
@@ -212,6 +228,27 @@ struct dcol_plan {
 
 namespace {
 
+// Stop a table's pair server, if one may be running: raise `stop` and wait for the server
+// stream to drain, at most timeout_ms.  false: it did not drain -- the wave may still read
+// the mailbox, which must then stay allocated.  The caller holds t->mu (or owns t).
+bool stop_pair_server(dcol_table* t, int timeout_ms) {
+    if (!t->server_launched || !t->pair_host) return true;
+    __atomic_store_n(&t->pair_host->stop, 1, __ATOMIC_SEQ_CST);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipStreamQuery(t->server_stream);
+        if (q != hipErrorNotReady) {
+            if (q != hipSuccess) (void)hipGetLastError();
+            break;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) return false;
+        std::this_thread::yield();
+    }
+    __atomic_store_n(&t->pair_host->stop, 0, __ATOMIC_SEQ_CST);
+    __atomic_store_n(&t->pair_host->alive, 0, __ATOMIC_SEQ_CST);
+    return true;
+}
+
 hipError_t launch_variant(int N, int nsoc, int omax, int lpp, int flags, const KArgs& a, hipStream_t st, int oe = 0) {
     if (oe > 0) {
         if (N == 5 && nsoc == 1) return launch_part_n5s1(omax, oe, lpp, flags, a, st);
@@ -292,17 +329,25 @@ int dcol_table_create(const dcol_shape_desc* shapes, int32_t n, int32_t device, 
     }
     t->shapes.resize(n);
     t->side_ready = device_side_streams(device, t->side);   // early: see DeviceSide
+    {
+        std::lock_guard<std::mutex> lk(g_tables_mu);
+        g_tables.push_back(t);
+    }
     *out = t;
     return DCOL_SUCCESS;
 }
 
 int dcol_table_destroy(dcol_table* t) {
     if (!t) return DCOL_SUCCESS;
-    DeviceGuard g(t->device);
-    if (t->server_launched) {   // the server exits at its next poll
-        __atomic_store_n(&t->pair_host->stop, 1, __ATOMIC_SEQ_CST);
-        (void)hipStreamSynchronize(t->server_stream);
+    {
+        std::lock_guard<std::mutex> lk(g_tables_mu);
+        g_tables.erase(std::remove(g_tables.begin(), g_tables.end(), t), g_tables.end());
     }
+    DeviceGuard g(t->device);
+    // the server exits at its next poll; one that does not (a hung device) keeps the whole
+    // table -- its wave may still read the shape table and the mailbox -- and the call fails
+    if (!stop_pair_server(t, kServerStopMs))
+        return fail(DCOL_ERR_HIP, "dcol_table_destroy: the pair server did not stop within 5 s (table leaked)");
     for (auto& kv : t->pair_lru) dcol_plan_destroy(kv.second);
     if (t->pair_stream) (void)hipStreamDestroy(t->pair_stream);
     if (t->server_stream) (void)hipStreamDestroy(t->server_stream);
@@ -902,15 +947,27 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
     std::lock_guard<std::mutex> lk(t->mu);
     DeviceGuard g(t->device);
     if (!t->pair_host) {
+        // fine-grained coherent on purpose: the server's handshake (system-scope atomics on
+        // req / done / alive / stop) needs host and device to see each other's stores while
+        // the wave runs, whatever HIP_HOST_COHERENT says
         hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&t->pair_host), sizeof(PairBox),
-                                     hipHostMallocMapped | hipHostMallocPortable);
+                                     hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent);
         if (e == hipSuccess) {
             std::memset(t->pair_host, 0, sizeof(PairBox));   // flags and sequence numbers start at 0
             t->pair_host->xcd = -1;                           // no server yet
         }
         if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&t->pair_dev), t->pair_host, 0);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&t->pair_stream, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&t->server_stream, hipStreamNonBlocking);
+        // The server stream at the device's highest priority: HIP pools hardware queues per
+        // priority level (GPU_MAX_HW_QUEUES each), so the resident server gets a queue of its
+        // own instead of sharing one with the caller's or the side streams, whose kernels
+        // would otherwise wait behind it until it idles out
+        int prio_lo = 0, prio_hi = 0;
+        if (e == hipSuccess && hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) {
+            (void)hipGetLastError();
+            prio_hi = 0;
+        }
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&t->server_stream, hipStreamNonBlocking, prio_hi);
         int khz = 0;
         if (e == hipSuccess && hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, t->device) != hipSuccess) {
             (void)hipGetLastError();
@@ -958,7 +1015,8 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
     // same solver copies) costs no launch.
     const int idle_us = pair_server_idle_us();
     const Launch& L0 = plan->launches[0];
-    int vid = (single && idle_us > 0 && t->wall_ticks_us > 0 && ns <= (1 << kPairBoxIdBits) && L0.lpp < 65536)
+    int vid = (single && idle_us > 0 && t->wall_ticks_us > 0 && ns <= (1 << kPairBoxIdBits) && L0.lpp < 65536 &&
+               !g_shutdown.load(std::memory_order_acquire))
                   ? fused_vid(L0.N, L0.nsoc, L0.omax, L0.lpp, L0.flags(), L0.oe) : -1;
     const int32_t kflags = flags & ~DCOL_CASE4;
     // Flags / tolerance / iteration cap are the server's launch arguments.  A call with others
@@ -1012,17 +1070,15 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
             h->flags = kflags;
             h->tol = tol;
             h->max_iter = max_iter;
+            // a resident wave must not outlive the process's HIP context: stop every server
+            // at exit (the handler runs before the HIP runtime's own, registered earlier)
+            std::call_once(g_exit_hook, [] { std::atexit([] { (void)dcol_shutdown(); }); });
             t->server_launched = true;
             ++t->n_starts;
             return launch_pair_server(a, d, (int64_t)idle_us * t->wall_ticks_us, t->server_stream);
         };
-        if (restart) {   // stop the running server (it leaves at its next poll), then start anew
-            __atomic_store_n(&h->stop, 1, __ATOMIC_SEQ_CST);
-            const hipError_t e = hipStreamSynchronize(t->server_stream);
-            __atomic_store_n(&h->stop, 0, __ATOMIC_SEQ_CST);
-            __atomic_store_n(&h->alive, 0, __ATOMIC_SEQ_CST);
-            if (e != hipSuccess) return fail(DCOL_ERR_HIP, std::string("dcol_prox_pair server: ") + hipGetErrorString(e));
-        }
+        if (restart && !stop_pair_server(t, kServerStopMs))   // it leaves at its next poll, then start anew
+            return fail(DCOL_ERR_HIP, "dcol_prox_pair: the pair server did not stop within 5 s");
         const uint32_t useq = (uint32_t)(h->req >> 32) + 1u;
         const int32_t seq = (int32_t)useq;
         h->ids = ((uint64_t)(useq & 0xffffu) << 48) | ((uint64_t)(uint32_t)s2 << kPairBoxIdBits) | (uint64_t)(uint32_t)s1;
@@ -1044,10 +1100,7 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
                 if (q == hipErrorNotReady && std::chrono::steady_clock::now() - t_post > std::chrono::seconds(30)) {
                     // a server that never answers (not expected: a solve takes microseconds):
                     // make it leave, so the next call starts clean, and report
-                    __atomic_store_n(&h->stop, 1, __ATOMIC_SEQ_CST);
-                    (void)hipStreamSynchronize(t->server_stream);
-                    __atomic_store_n(&h->stop, 0, __ATOMIC_SEQ_CST);
-                    __atomic_store_n(&h->alive, 0, __ATOMIC_SEQ_CST);
+                    (void)stop_pair_server(t, kServerStopMs);
                     return fail(DCOL_ERR_HIP, "dcol_prox_pair: the pair server did not answer within 30 s");
                 }
                 if (q == hipSuccess && __atomic_load_n(&h->done, __ATOMIC_ACQUIRE) != seq) {
@@ -1085,6 +1138,50 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
     if (iters) *iters = h->iters;
     if (status) *status = h->status;
     return DCOL_SUCCESS;
+}
+
+int dcol_table_stop_pair_server(const dcol_table* tc) {
+    if (!tc) return fail(DCOL_ERR_ARG, "dcol_table_stop_pair_server: NULL table");
+    dcol_table* t = const_cast<dcol_table*>(tc);
+    std::lock_guard<std::mutex> lk(t->mu);
+    DeviceGuard g(t->device);
+    if (!stop_pair_server(t, kServerStopMs))
+        return fail(DCOL_ERR_HIP, "dcol_table_stop_pair_server: the pair server did not stop within 5 s");
+    return DCOL_SUCCESS;
+}
+
+int dcol_table_pair_server_running(const dcol_table* tc, int32_t* running) {
+    if (!tc || !running) return fail(DCOL_ERR_ARG, "dcol_table_pair_server_running: NULL argument");
+    dcol_table* t = const_cast<dcol_table*>(tc);
+    std::lock_guard<std::mutex> lk(t->mu);
+    DeviceGuard g(t->device);
+    *running = 0;
+    if (t->server_launched) {
+        const hipError_t q = hipStreamQuery(t->server_stream);
+        if (q == hipErrorNotReady)
+            *running = 1;
+        else if (q != hipSuccess)
+            return fail(DCOL_ERR_HIP, std::string("dcol_table_pair_server_running: ") + hipGetErrorString(q));
+    }
+    return DCOL_SUCCESS;
+}
+
+int dcol_shutdown(void) {
+    g_shutdown.store(true, std::memory_order_release);
+    std::lock_guard<std::mutex> lk(g_tables_mu);
+    int running = 0, stuck = 0;
+    for (dcol_table* t : g_tables) {
+        std::lock_guard<std::mutex> tl(t->mu);
+        if (!t->server_launched) continue;
+        DeviceGuard g(t->device);
+        if (hipStreamQuery(t->server_stream) == hipErrorNotReady) ++running;
+        (void)hipGetLastError();
+        if (!stop_pair_server(t, kServerStopMs)) ++stuck;
+    }
+    if (const char* dbg = std::getenv("DCOL_DEBUG_SHUTDOWN"); dbg && *dbg && *dbg != '0')
+        std::fprintf(stderr, "dcol_shutdown: %zu tables, %d pair servers running, %d stopped, %d did not stop\n",
+                     g_tables.size(), running, running - stuck, stuck);
+    return stuck ? fail(DCOL_ERR_HIP, "dcol_shutdown: a pair server did not stop within 5 s") : DCOL_SUCCESS;
 }
 
 int dcol_table_pair_plans(const dcol_table* tc, int32_t* n) {

@@ -5,6 +5,7 @@ every entry point raises :class:`DcolLibraryError` (loudly, with the reason).
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_void_p
@@ -64,6 +65,9 @@ SIGNATURES = {
     "dcol_table_pair_plans": (c_int, [c_void_p, POINTER(c_int32)]),
     "dcol_table_pair_stats": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64),
                                       POINTER(c_double), POINTER(c_double), POINTER(c_int32)]),
+    "dcol_table_stop_pair_server": (c_int, [c_void_p]),
+    "dcol_table_pair_server_running": (c_int, [c_void_p, POINTER(c_int32)]),
+    "dcol_shutdown": (c_int, []),
     "dcol_comm_unique_id": (c_int, [c_void_p]),
     "dcol_comm_create": (c_int, [c_void_p, c_int32, c_int32, c_int32, POINTER(c_void_p)]),
     "dcol_comm_destroy": (c_int, [c_void_p]),
@@ -100,7 +104,16 @@ def load(path: str | None = None):
         raise DcolLibraryError(f"{p}: ABI version {lib.dcol_abi_version()} != {ABI_VERSION}")
     if path is None:
         _lib = lib
+        # stop every resident pair server before interpreter teardown: Table.__del__ (which
+        # would stop its table's) is not guaranteed to run at exit.  The library's own exit
+        # handler does the same later; this one runs while Python still owns its threads.
+        atexit.register(_shutdown)
     return lib
+
+
+def _shutdown():
+    if _lib is not None:
+        _lib.dcol_shutdown()
 
 
 def check(rc: int, what: str = ""):

@@ -14,6 +14,12 @@ batch order within each class.
 """
 from __future__ import annotations
 
+import json
+import os
+import sys
+import threading
+import time
+
 import numpy as np
 
 REC = 14   # packed record per pair: alpha, grad[12] (float64), then (status, iters) as two int32
@@ -226,3 +232,83 @@ class NativeComm:
             self.close()
         except Exception:
             pass
+
+
+class StepWatchdog:
+    """Host-side deadline for one rank of a multi-rank run (bench.py --gpus N > 1).
+
+    The main thread names what it is about to wait for -- ``arm(phase, step)`` before a
+    collective, a barrier or a wait for a step's completion event -- and ``disarm()`` after.
+    A daemon thread that finds an armed deadline passed prints ONE JSON line to stderr
+    ({"dcol_deadline": true, "rank", "world", "phase", "step", "waited_s", "deadline_s"}) and
+    ends the process with ``exit_code`` through os._exit: no interpreter teardown, which could
+    itself block in the collective that hung.  The launcher (torchrun) then stops the other
+    ranks.  It never re-executes anything.  A hang in a native call (RCCL, a HIP stream wait)
+    is caught as well as one in Python, since every such call releases the GIL."""
+
+    def __init__(self, rank: int, world: int, deadline_s: float = 120.0, exit_code: int = 3, poll_s: float = 0.05):
+        self.rank, self.world = int(rank), int(world)
+        self.deadline_s = float(deadline_s)
+        self.exit_code = int(exit_code)
+        self._poll = float(poll_s)
+        self._lock = threading.Lock()
+        self._armed = None          # (phase, step, t0, seconds)
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._watch, name="dcol-step-watchdog", daemon=True)
+        self._thread.start()
+
+    def arm(self, phase: str, step=None, seconds=None):
+        with self._lock:
+            self._armed = (str(phase), None if step is None else int(step), time.monotonic(),
+                           self.deadline_s if seconds is None else float(seconds))
+
+    def disarm(self):
+        with self._lock:
+            self._armed = None
+
+    def guard(self, phase: str, step=None, seconds=None):
+        """context manager: arm on entry, disarm on exit"""
+        wd = self
+
+        class _G:
+            def __enter__(self_):
+                wd.arm(phase, step, seconds)
+
+            def __exit__(self_, *exc):
+                wd.disarm()
+                return False
+        return _G()
+
+    def wait_event(self, event, phase: str, step=None, seconds=None):
+        """wait for a torch.cuda.Event (polling query(), so the wait itself never blocks
+        the interpreter) under the deadline"""
+        self.arm(phase, step, seconds)
+        while not event.query():
+            time.sleep(0)
+        self.disarm()
+
+    def close(self):
+        self._stop.set()
+        self._thread.join(timeout=1.0)
+
+    def _watch(self):
+        while not self._stop.wait(self._poll):
+            with self._lock:
+                a = self._armed
+            if a is None:
+                continue
+            phase, step, t0, seconds = a
+            waited = time.monotonic() - t0
+            if waited > seconds:
+                self._fire(phase, step, waited, seconds)
+
+    def _fire(self, phase, step, waited, seconds):
+        line = {"dcol_deadline": True, "rank": self.rank, "world": self.world, "phase": phase, "step": step,
+                "waited_s": round(waited, 3), "deadline_s": seconds,
+                "note": "this rank waited past its deadline; exiting non-zero (the launcher stops the other ranks)"}
+        try:
+            sys.stderr.write(json.dumps(line) + "\n")
+            sys.stderr.flush()
+            sys.stdout.flush()
+        finally:
+            os._exit(self.exit_code)

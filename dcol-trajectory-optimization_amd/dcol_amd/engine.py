@@ -353,7 +353,10 @@ class Engine:
             h1 = self._obj_ids.get(id(prim1))
             h2 = self._obj_ids.get(id(prim2))
             fast = _fastpair()
-            if fast is not None and h1 is not None and h2 is not None and h1[0] is prim1 and h2[0] is prim2:
+            # (an id past this table's size belongs to the next table, which another thread's
+            # register_object has just invalidated this one for: the locked path rebuilds)
+            if (fast is not None and h1 is not None and h2 is not None and h1[0] is prim1 and h2[0] is prim2
+                    and h1[1] < table.n and h2[1] < table.n):
                 r = fast[0](fast[1], table.handle.value, h1[1], h2[1], prim1.r, prim1.p, prim2.r, prim2.p, tol,
                             self.max_iter, flags, contact)
                 if r is not None:
@@ -379,6 +382,22 @@ class Engine:
                 _lib.check(rc, "dcol_prox_pair")
             return (np.float64(alpha[0]), cp.copy() if contact else None, g.copy() if flags & _lib.GRAD_ANY else None,
                     int(ints[0]), int(ints[1]))
+
+    def stop_pair_server(self):
+        """dcol_table_stop_pair_server: the table's resident pair server leaves now (the next
+        solve_pair starts a new one)"""
+        with self._lock:
+            if self._table is not None:
+                _lib.check(_lib.load().dcol_table_stop_pair_server(self._table.handle), "dcol_table_stop_pair_server")
+
+    def pair_server_running(self) -> bool:
+        with self._lock:
+            if self._table is None:
+                return False
+            v = ctypes.c_int32()
+            _lib.check(_lib.load().dcol_table_pair_server_running(self._table.handle, ctypes.byref(v)),
+                       "dcol_table_pair_server_running")
+            return bool(v.value)
 
     def pair_stats(self):
         """dcol_table_pair_stats of the current table: {"served": calls the one-pair server

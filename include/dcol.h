@@ -39,7 +39,7 @@ extern "C" {
 
 #define DCOL_ABI_VERSION 3   /* 2: 14-slot multi-GPU record (status / iters as an int32 pair);
                                 3: DCOL_NO_GATHER + dcol_comm_all_gather, dcol_table_pair_plans,
-                                   dcol_table_pair_stats */
+                                   dcol_table_pair_stats; dcol_shutdown */
 
 /* Primitive types (misc_primitive_constructor.py:4-88). */
 enum dcol_shape_type {
@@ -197,7 +197,9 @@ int dcol_prox_batch_host(const dcol_table* table, int64_t B, const int32_t* shap
  * variant the fused small-plan kernel has is served by the table's one-pair SERVER: one
  * resident workgroup polling that memory, started by the first such call and leaving after
  * DCOL_PAIR_SERVER_IDLE_US (default 1000) without a request -- no kernel launch per call.
- * (A device-wide synchronisation issued meanwhile waits for it to leave.)  Other pairs,
+ * (A device-wide synchronisation issued meanwhile waits for it to leave.  The server runs
+ * on a stream of the device's highest priority, so it holds a hardware queue of its own and
+ * no kernel of another stream queues behind it.)  Other pairs,
  * and every pair under DCOL_PAIR_SERVER=0, take one launch on a stream of the table.
  * Calls on one table are serialised.                                                      */
 int dcol_prox_pair(const dcol_table* table, int32_t shape1, int32_t shape2, const double* pose1,
@@ -215,6 +217,21 @@ int dcol_table_pair_plans(const dcol_table* table, int32_t* n);
 int dcol_table_pair_stats(const dcol_table* table, int64_t* served, int64_t* launched,
                           int64_t* server_starts, double* server_solve_us, double* server_solve_cycles,
                           int32_t* server_xcd);
+
+/* Stop this table's pair server now, if one is resident (waiting at most 5 s for it to
+ * leave); the next dcol_prox_pair starts a new one.  E.g. before a long batch phase, so no
+ * wave polls the mailbox meanwhile.                                                      */
+int dcol_table_stop_pair_server(const dcol_table* table);
+/* *running = 1 while this table's pair server is resident (its stream has not drained).  */
+int dcol_table_pair_server_running(const dcol_table* table, int32_t* running);
+/* Stop every resident pair server of the process (each table's, waiting at most 5 s for
+ * each to leave) and start no new one: later dcol_prox_pair calls take the launch path.
+ * Registered as an exit handler at the first server start, so a process that exits without
+ * destroying its tables never tears down its HIP context under a polling wave; callers may
+ * also run it themselves before their own teardown (the Python binding does, at atexit).
+ * DCOL_DEBUG_SHUTDOWN=1 reports the servers it found running on stderr.  Returns
+ * DCOL_ERR_HIP if a server did not leave (its table is then kept).                      */
+int dcol_shutdown(void);
 
 /* ---- multi-GPU ------------------------------------------------------
  * One process per GPU.  Pairs are independent, so each rank solves its own shard with its

@@ -194,3 +194,44 @@ def test_native_comm_solve_gather_argument_combinations():
         comm.solve_gather(_Plan(), None, None, 4, rec_local=object(), in_place=True)
     with pytest.raises(ValueError, match="soa=False"):
         comm.solve_gather(_Plan(), None, None, 4, soa=False)
+
+
+def _run_deadline(mode, deadline=3.0, timeout=120):
+    import json
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(here, "deadline_rank.py"), mode, str(deadline)]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
+    diags = []
+    for ln in (p.stderr + p.stdout).splitlines():
+        i = ln.find('{"dcol_deadline"')
+        if i >= 0:
+            diags.append(json.loads(ln[i:]))
+    return p, diags
+
+
+def test_deadline_rank_skipping_a_step_exits_nonzero_with_diagnostic():
+    """bench.py's N > 1 deadline (dcol_amd.dist.StepWatchdog): rank 1 skips step 2 of the
+    all-gather loop and stalls; rank 0, waiting in step 2's all-gather, must print ONE JSON
+    diagnostic naming its rank, the phase and the step, and the run must exit non-zero well
+    before the backend's own timeout -- instead of hanging until the launcher's limit."""
+    import time
+    t0 = time.monotonic()
+    p, diags = _run_deadline("skip", deadline=3.0)
+    took = time.monotonic() - t0
+    assert p.returncode != 0, p.stdout + p.stderr
+    r0 = [d for d in diags if d["rank"] == 0]
+    assert r0, p.stderr[-3000:]
+    assert r0[0]["phase"] == "all-gather" and r0[0]["step"] == 2 and r0[0]["world"] == 2
+    assert r0[0]["waited_s"] >= 3.0
+    assert took < 60, took        # the backend's own timeout is 90 s
+
+
+def test_deadline_clean_run_exits_zero():
+    p, diags = _run_deadline("none", deadline=20.0)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert not diags
+    assert p.stdout.count("steps done") == 2

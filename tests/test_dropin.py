@@ -340,3 +340,120 @@ def test_pair_server_two_threads(engine):
         for r in rs:
             np.testing.assert_array_equal(_bits([r]), _bits([ref[i]]))
         assert alpha_close(rs[0][0], d["alpha"][i]) and grad_close(rs[0][2], d["grad"][i])
+
+
+def _child(mode, env_extra, timeout=240):
+    import os
+    import subprocess
+    import sys
+    import time
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, **env_extra)
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, os.path.join(here, "server_exit_child.py"), mode], capture_output=True,
+                       text=True, timeout=timeout, env=env)
+    return p, time.monotonic() - t0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["python", "c"])
+def test_pair_server_stopped_at_process_exit(mode):
+    """A process that makes drop-in calls and exits without destroying its tables while the
+    one-pair server is resident (idle time 60 s): the server is stopped at exit -- by the
+    binding's atexit hook (dcol_amd/_lib.py) or, with that unregistered, by the library's
+    own exit handler (dcol_shutdown, registered at the first server start) -- so the process
+    neither tears its HIP context down under a polling wave nor waits out the idle time.
+    Then a fresh process opens the device, solves pairs and stops its own server."""
+    env = {"DCOL_PAIR_SERVER": "1", "DCOL_PAIR_SERVER_IDLE_US": "60000000", "DCOL_DEBUG_SHUTDOWN": "1"}
+    p, took = _child(mode, env)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "CHILD_OK" in p.stdout and "running=1" in p.stdout, p.stdout + p.stderr
+    reports = [ln for ln in p.stderr.splitlines() if ln.startswith("dcol_shutdown:")]
+    # the first dcol_shutdown of the exit found the resident server and stopped it
+    assert reports and "1 pair servers running, 1 stopped, 0 did not stop" in reports[0], p.stderr
+    assert len(reports) == (2 if mode == "python" else 1), reports
+    assert took < 45, took       # the idle time (60 s) was not waited out
+    q, _ = _child("reopen", {"DCOL_PAIR_SERVER": "1", "DCOL_DEBUG_SHUTDOWN": "1"})
+    assert q.returncode == 0, q.stdout + q.stderr
+    assert "CHILD_OK mode=reopen" in q.stdout and "served=" in q.stdout, q.stdout + q.stderr
+    alpha = lambda out: float(out.split("alpha0=")[1].split()[0].replace("np.float64(", "").rstrip(")"))  # noqa: E731
+    assert alpha(p.stdout) == alpha(q.stdout)
+
+
+@pytest.mark.gpu
+def test_pair_server_does_not_tax_batch_plan(engine, monkeypatch):
+    """A batch plan (100k poly x poly pairs, bench configs[3]) run while the one-pair server
+    is resident takes the same time as with it stopped (the server has its own
+    highest-priority hardware queue and one CU), and returns bitwise the same results; the
+    drop-in's launch path (a call with other flags) while the server is resident as well.
+    The measured figures are printed (tools/server_tax.py records them)."""
+    import torch
+    from bench import pairs, shape_table
+    from dcol_amd import alloc_outputs, spec_from_arrays
+    from primitives.misc_primitive_constructor import SphereMRP, create_rect_prism
+    monkeypatch.setenv("DCOL_PAIR_SERVER", "1")
+    monkeypatch.setenv("DCOL_PAIR_SERVER_IDLE_US", "30000000")
+    tab = shape_table()
+    ids = np.array([engine.register(spec_from_arrays(tab, k)) for k in range(len(tab["type"]))], np.int32)
+    box = create_rect_prism(1.0, 2.0, 0.5)
+    ball = SphereMRP(0.4)
+    box.r, box.p = np.zeros(3), np.array([0.1, -0.2, 0.3])
+    ball.r, ball.p = np.array([2.0, 0.5, -0.3]), np.zeros(3)
+    engine.solve_pair(ball, box, grad=None)           # registers both: the table is final now
+    B = 100_000
+    s1, s2, p1, p2 = pairs(B, len(tab["type"]), seed=3)
+    plan = engine.plan(ids[s1], ids[s2], cache=False)
+    dev = torch.device("cuda", engine.device)
+    d1 = torch.from_numpy(np.ascontiguousarray(p1.T)).to(dev)
+    d2 = torch.from_numpy(np.ascontiguousarray(p2.T)).to(dev)
+    out = alloc_outputs(B, dev, want_grad=True, want_contact=False)
+    stream = torch.cuda.current_stream(dev)
+    run = plan.bind(d1, d2, out, grad="fd", contact=False, stream=stream)
+
+    def timed(n=40):
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+        for a, b in ev:
+            a.record(stream)
+            run()
+            b.record(stream)
+        ev[-1][1].synchronize()
+        return float(np.median([a.elapsed_time(b) for a, b in ev]))
+
+    for _ in range(60):                               # clocks up
+        run()
+    stream.synchronize()
+    ref = {k: v.clone() for k, v in out.items()}
+    t = {"stopped": [], "resident": []}
+    for rep in range(3):
+        engine.stop_pair_server()
+        assert not engine.pair_server_running()
+        t["stopped"].append(timed())
+        engine.solve_pair(ball, box, grad=None)       # the server is resident (30 s idle)
+        assert engine.pair_server_running()
+        t["resident"].append(timed())
+        assert engine.pair_server_running()
+        for k, v in out.items():
+            assert torch.equal(v, ref[k]), k
+    # the launch path while the server is resident: a call with other flags
+    lat = {}
+    import time
+    for state in ("resident", "stopped"):
+        if state == "stopped":
+            monkeypatch.setenv("DCOL_PAIR_SERVER", "0")
+            engine.stop_pair_server()
+        else:
+            engine.solve_pair(ball, box, grad=None)
+        ts = []
+        for _ in range(50):
+            t0 = time.perf_counter()
+            engine.solve_pair(ball, box, grad="envelope")    # mismatching flags: launched
+            ts.append(time.perf_counter() - t0)
+            if state == "resident":
+                engine.solve_pair(ball, box, grad=None)      # (served: keeps the server's flags)
+        lat[state] = 1e6 * float(np.median(ts))
+    engine.stop_pair_server()
+    stopped, resident = min(t["stopped"]), min(t["resident"])
+    print(f"server_tax: batch ms stopped {t['stopped']} resident {t['resident']} ratio {resident / stopped:.4f}; "
+          f"launch-path us resident {lat['resident']:.1f} stopped {lat['stopped']:.1f}")
+    assert resident / stopped < 1.10, t
+    assert lat["resident"] < 3 * lat["stopped"] + 50, lat

@@ -17,7 +17,8 @@ import subprocess
 import sys
 import tempfile
 
-CSRC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "dcol-trajectory-optimization_amd", "csrc")
+CSRC = os.environ.get("DCOL_ISA_CSRC",   # (another copy of the sources, e.g. an experiment's)
+                      os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "dcol-trajectory-optimization_amd", "csrc"))
 
 SRC = """#include "dcol_device.hpp"
 namespace dcol {{
