@@ -206,6 +206,10 @@ def main():
                     help="N > 1: the longest any rank waits for one phase (communicator set-up, a step's solve, its "
                          "all-gather, a barrier) before it prints a JSON diagnostic (rank, step, phase) to stderr and "
                          "exits non-zero (dcol_amd.dist.StepWatchdog)")
+    ap.add_argument("--settle-ms", type=float, default=30.0,
+                    help="before the warm-up, run the step until this much GPU time has passed (HIP events), so the "
+                         "timed steps do not run on the GPU's clock ramp (the clocks settle after ~15 ms of sustained "
+                         "load, DESIGN.md section 0); reported in the line as `settle`; 0 = off")
     ap.add_argument("--pack-pass", action="store_true",
                     help="mixed1m: per-pair arrays + pack_records kernel + out-of-place all-gather instead of "
                          "records written by the solver kernels with the all-gather in place (A/B)")
@@ -280,6 +284,7 @@ def main():
                                 grad=args.grad, contact=False, stream=st, max_iter=args.max_iter)
                       for st in lane_streams[1:]]
 
+    settle = clock_settle(step, stream, dev, wd, args.settle_ms)
     for k in range(args.warmup):
         step()
     sync(dev, wd, "warmup")
@@ -389,6 +394,7 @@ def main():
                      "value": (B * world * args.steps / elapsed_pipe) if elapsed_pipe else None,
                      "ms_per_step": 1e3 * elapsed_pipe / args.steps if elapsed_pipe else None},
         "kernel_ms_max_rank": kern_ms_max,
+        "settle": settle,
         "world": {"ranks": world, "process_group_size": dist.get_world_size() if dist is not None else 1,
                   "backend": args.backend if dist is not None else None, "devices_visible": ndev},
         "solve_stats": {"ok_frac": float(np.mean(status == 0)), "iters_mean": float(iters[status == 0].mean()),
@@ -457,6 +463,31 @@ def summary(line):
     if "cpu_baseline" in line:
         out["cpu_baseline"] = line["cpu_baseline"]["value"]
     return out
+
+
+def clock_settle(step, stream, dev, wd, ms):
+    """Run `step` in rounds of 10 until `ms` of GPU time (HIP events on its stream) has
+    passed: the GPU's clocks ramp up over the first ~15 ms of sustained load
+    (profiles/r04_clock/), and a short timed run (the driver's --steps 20) would otherwise be
+    measured on the ramp.  Untimed, outside the W warm-up steps and the K timed ones; the
+    line reports what it ran."""
+    import torch
+    done, steps = 0.0, 0
+    while done < ms:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(10):
+            step()
+        e1.record(stream)
+        if wd is None:
+            e1.synchronize()
+        else:
+            wd.wait_event(e1, "clock settle")
+        done += e0.elapsed_time(e1)
+        steps += 10
+    return {"gpu_ms": done, "steps": steps,
+            "note": "untimed steps before the warm-up until this much GPU time had passed (--settle-ms): the timed "
+                    "steps run at settled clocks, not on the ramp"}
 
 
 def guard(wd, phase, step=None):
@@ -834,6 +865,7 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup, 
             el = float(t[0])
         return el, marks
 
+    settle = clock_settle(launch, stream, dev, wd, args.settle_ms)
     elapsed, marks = run_steps([step], "serial")
     # the solve's share of each timed step (start -> solved) and the whole step, same run
     kernel_ms = float(np.median([a.elapsed_time(b) for a, b, _ in marks]))
@@ -918,6 +950,7 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup, 
                          "kernel_ms": ranks_stats[:, 4].tolist(), "plan_run_ms": ranks_stats[:, 5].tolist(),
                          "iters_mean": ranks_stats[:, 2].tolist(), "pairs": ranks_stats[:, 3].astype(int).tolist()}},
         "kernel_ms_max_rank": float(ranks_stats[:, 4].max()),
+        "settle": settle,
         "pipeline": {"streams": max(1, len(lanes)), "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                      "note": "solves round-robin on the streams, all-gathers on one collective stream (an overlap "
                              "rate, not value)",

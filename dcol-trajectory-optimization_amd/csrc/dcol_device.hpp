@@ -637,7 +637,7 @@ struct Grp<4> {
 // 4 or 3 instead of 6, and it holds 4 or 3 doubles of G instead of 6.  The rows' reference
 // order within a pair changes, i.e. the lane sums add the same terms in another order
 // (rounding level); parity is pinned by iteration-count equality on every golden vector.
-template <int N, int NSOC, int OMAX, int LPP, bool BALL = false, bool CONE = false, int OE = 0>
+template <int N, int NSOC, int OMAX, int LPP, bool BALL = false, bool CONE = false, int OE = 0, bool GLDS = false>
 struct Solver {
     static_assert(OMAX % LPP == 0, "OMAX must be a multiple of LPP");
     static_assert(!(BALL && CONE) && (!CONE || N == 4), "CONE: cone-only SOC blocks of N = 4 pairs");
@@ -655,9 +655,65 @@ struct Solver {
     static constexpr int NXA = NX > 0 ? NX : 1;
     using R = Grp<LPP>;
 
-    double G[MG][N];
+    // GLDS ("LDS rows", variants.py): G and the CONE rows live in this lane's column of a
+    // per-workgroup LDS array instead of registers -- they are constant through the PDIP loop
+    // and read a few times per iteration -- so the kernel fits fewer VGPRs (no AGPR parking,
+    // two waves per SIMD for the one-lane cone x polytope kernel).  Compact layout (gidx):
+    // a PART pose slot stores columns 0..3, an extra-column slot columns 3..N-1, any other row
+    // all N; the CONE rows follow (10 per slot).  The LDS pointer is laundered at the PDIP
+    // phase boundaries (grefresh), so no load is hoisted out of its phase and held in
+    // registers across the loop (which would undo the point).  Same arithmetic in the same
+    // order as the register form: bitwise equal results (the codegen-invariance twin is built
+    // without LDS rows, tests/test_gpu_fullsize.py).
+#if defined(__HIP_DEVICE_COMPILE__)
+    using lds_d = __attribute__((address_space(3))) double;
+#else
+    using lds_d = double;
+#endif
+    DCOL_HD static constexpr int gidx(int k, int j) {
+        if constexpr (PART) {
+            if (k < PL) return 4 * k + j;
+            if (k < OR) return 4 * PL + (N - 3) * (k - PL) + (j - 3);
+            return 4 * PL + (N - 3) * EL + N * (k - OR) + j;
+        }
+        return N * k + j;
+    }
+    static constexpr int GW = PART ? 4 * PL + (N - 3) * EL + N * (MG - OR) : MG * N;   // doubles of G
+    static constexpr int LDSW = GW + (CONE ? 10 * SSA : 0);   // doubles per lane in LDS (GLDS)
+    static constexpr int kLdsStride = 64;                     // lanes per workgroup (kSolveBlock)
+    double G[GLDS ? 1 : MG][N];
     double sv[SSA], sR[SSA], sX[SSA][3][NXA];   // BALL: structured SOC rows (see above)
-    double cq[SSA][3][3], cc0[SSA];             // CONE: row e of slot b = [cq[b][e] | e == 0 ? cc0[b] : 0]
+    double cq[GLDS ? 1 : SSA][3][3], cc0[GLDS ? 1 : SSA];   // CONE: row e of slot b = [cq[b][e] | e == 0 ? cc0[b] : 0]
+    mutable lds_d* gb = nullptr;                // GLDS: this lane's first element
+    DCOL_HD decltype(auto) gx(int k, int j) const {
+        if constexpr (GLDS) return (gb[gidx(k, j) * kLdsStride]);
+        else return (G[k][j]);
+    }
+    DCOL_HD decltype(auto) gx(int k, int j) {
+        if constexpr (GLDS) return (gb[gidx(k, j) * kLdsStride]);
+        else return (G[k][j]);
+    }
+    DCOL_HD decltype(auto) cqx(int b, int e, int c) const {
+        if constexpr (GLDS) return (gb[(GW + 10 * b + 3 * e + c) * kLdsStride]);
+        else return (cq[b][e][c]);
+    }
+    DCOL_HD decltype(auto) cqx(int b, int e, int c) {
+        if constexpr (GLDS) return (gb[(GW + 10 * b + 3 * e + c) * kLdsStride]);
+        else return (cq[b][e][c]);
+    }
+    DCOL_HD decltype(auto) ccx(int b) const {
+        if constexpr (GLDS) return (gb[(GW + 10 * b + 9) * kLdsStride]);
+        else return (cc0[b]);
+    }
+    DCOL_HD decltype(auto) ccx(int b) {
+        if constexpr (GLDS) return (gb[(GW + 10 * b + 9) * kLdsStride]);
+        else return (cc0[b]);
+    }
+    DCOL_HD void grefresh() const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        if constexpr (GLDS) asm volatile("" : "+v"(gb));
+#endif
+    }
     double s[M], z[M], r[M];   // slack, dual, primal residual G x - h
     double x[N];
     double vimp[N];            // implicit-gradient mode: H^-1 e3 at the returned iterate
@@ -702,11 +758,11 @@ struct Solver {
         const double u0 = F.Qe[0] * a0 + F.Qe[1] * a1 + F.Qe[2] * a2;
         const double u1 = F.Qe[3] * a0 + F.Qe[4] * a1 + F.Qe[5] * a2;
         const double u2 = F.Qe[6] * a0 + F.Qe[7] * a1 + F.Qe[8] * a2;
-        G[k][0] = u0; G[k][1] = u1; G[k][2] = u2; G[k][3] = g3;
+        gx(k, 0) = u0; gx(k, 1) = u1; gx(k, 2) = u2; gx(k, 3) = g3;
         const int off = xoff(p2);
 #pragma unroll
         for (int j = 4; j < N; ++j)
-            if (nz(k, j)) G[k][j] = excol(j, off, e0, e1);
+            if (nz(k, j)) gx(k, j) = excol(j, off, e0, e1);
         r[k] = u0 * F.re[0] + u1 * F.re[1] + u2 * F.re[2];
     }
     // PART: one extra-column slot (pose-independent row [0 0 0, g3, ex], h = 0)
@@ -714,9 +770,9 @@ struct Solver {
         const double2* rw = reinterpret_cast<const double2*>(rows + 8 * (int64_t)(v ? ri : 0));
         const double2 q1 = rw[1], q2 = rw[2];
         const double g3 = q1.y, e0 = q2.x, e1 = q2.y;
-        G[k][3] = g3;
+        gx(k, 3) = g3;
 #pragma unroll
-        for (int j = 4; j < N; ++j) G[k][j] = excol(j, 0, e0, e1);
+        for (int j = 4; j < N; ++j) gx(k, j) = excol(j, 0, e0, e1);
         r[k] = 0.0;
     }
     // leaves h in r[] (init turns it into G x_hat - h)
@@ -798,22 +854,27 @@ struct Solver {
                 // row 0 column 3 cc = -(tanb 3H/4), h = -E Qe' re; the same products as
                 // soc_rows; an inert slot holds zero rows
                 const double tb = p2 ? S2.tanb : S1.tanb;
-                cc0[b] = vs[b] ? (p2 ? S2.cone_c : S1.cone_c) : 0.0;
+                ccx(b) = vs[b] ? (p2 ? S2.cone_c : S1.cone_c) : 0.0;
 #pragma unroll
                 for (int k = 0; k < 3; ++k) {
                     const double e = (k == 0) ? tb : 1.0;
                     const double u0 = -(e * Qe[0 + k]);
                     const double u1 = -(e * Qe[3 + k]);
                     const double u2 = -(e * Qe[6 + k]);
-                    cq[b][k][0] = vs[b] ? u0 : 0.0;
-                    cq[b][k][1] = vs[b] ? u1 : 0.0;
-                    cq[b][k][2] = vs[b] ? u2 : 0.0;
+                    cqx(b, k, 0) = vs[b] ? u0 : 0.0;
+                    cqx(b, k, 1) = vs[b] ? u1 : 0.0;
+                    cqx(b, k, 2) = vs[b] ? u2 : 0.0;
                     r[OR + SD * b + k] = vs[b] ? u0 * re[0] + u1 * re[1] + u2 * re[2] : 0.0;
                 }
                 (void)kind;
             } else {
+                double Gb[4][N];
                 soc_rows(kind, p2 ? S2.R : S1.R, p2 ? S2.cone_c : S1.cone_c, p2 ? S2.tanb : S1.tanb,
-                         p2 ? S2.n_extra : S1.n_extra, xoff(p2), Qe, re, &G[OR + SD * b], &r[OR + SD * b]);
+                         p2 ? S2.n_extra : S1.n_extra, xoff(p2), Qe, re, Gb, &r[OR + SD * b]);
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int j = 0; j < N; ++j) gx(OR + SD * b + e, j) = Gb[e][j];
             }
         }
     }
@@ -874,14 +935,14 @@ struct Solver {
         if constexpr (PART)
             if (k < OR) {   // the slot's structural nonzeros only
                 const int j0 = k < PL ? 0 : 3, j1 = k < PL ? 4 : N;
-                double acc = G[k][j0] * v[j0];
+                double acc = gx(k, j0) * v[j0];
 #pragma unroll
-                for (int j = j0 + 1; j < j1; ++j) acc += G[k][j] * v[j];
+                for (int j = j0 + 1; j < j1; ++j) acc += gx(k, j) * v[j];
                 return acc;
             }
-        double acc = G[k][0] * v[0];
+        double acc = gx(k, 0) * v[0];
 #pragma unroll
-        for (int j = 1; j < N; ++j) acc += G[k][j] * v[j];
+        for (int j = 1; j < N; ++j) acc += gx(k, j) * v[j];
         return acc;
     }
     // BALL: row e of SOC slot b times v
@@ -898,10 +959,10 @@ struct Solver {
     // CONE: row e of SOC slot b times v (the dense row's nonzero terms, same order)
     DCOL_HD double cone_row(int k, const double* v) const {
         const int b = (k - OR) / SD, e = (k - OR) % SD;
-        double acc = cq[b][e][0] * v[0];
-        acc += cq[b][e][1] * v[1];
-        acc += cq[b][e][2] * v[2];
-        if (e == 0) acc += cc0[b] * v[3];
+        double acc = cqx(b, e, 0) * v[0];
+        acc += cqx(b, e, 1) * v[1];
+        acc += cqx(b, e, 2) * v[2];
+        if (e == 0) acc += ccx(b) * v[3];
         return acc;
     }
     // out += G_b' v over the rows of SOC slot b (dense or structured)
@@ -911,8 +972,8 @@ struct Solver {
 #pragma unroll
             for (int e = 0; e < 3; ++e) {
 #pragma unroll
-                for (int j = 0; j < 3; ++j) out[j] += cq[b][e][j] * v[e];
-                if (e == 0) out[3] += cc0[b] * v[0];
+                for (int j = 0; j < 3; ++j) out[j] += cqx(b, e, j) * v[e];
+                if (e == 0) out[3] += ccx(b) * v[0];
             }
         } else if constexpr (BALL) {
 #pragma unroll
@@ -926,7 +987,7 @@ struct Solver {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
-                for (int j = 0; j < N; ++j) out[j] += G[k0 + e][j] * v[e];
+                for (int j = 0; j < N; ++j) out[j] += gx(k0 + e, j) * v[e];
         }
     }
     // gt = W^-1 G_b (SD x N), the SOC block of G~ (NT_scaling.py:164-202)
@@ -937,7 +998,7 @@ struct Solver {
             for (int j = 0; j < N; ++j) {
                 double col[3], res[3];
 #pragma unroll
-                for (int e = 0; e < 3; ++e) col[e] = (j < 3) ? cq[b][e][j] : (e == 0 ? cc0[b] : 0.0);
+                for (int e = 0; e < 3; ++e) col[e] = (j < 3) ? cqx(b, e, j) : (e == 0 ? ccx(b) : 0.0);
                 soc_solve<3>(W, col, res);
 #pragma unroll
                 for (int e = 0; e < 3; ++e) gt[e][j] = res[e];
@@ -968,7 +1029,7 @@ struct Solver {
             for (int j = 0; j < N; ++j) {
                 double col[4], res[4];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) col[e] = G[k0 + e][j];
+                for (int e = 0; e < 4; ++e) col[e] = gx(k0 + e, j);
                 soc_solve(W, col, res);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) gt[e][j] = res[e];
@@ -1173,10 +1234,10 @@ struct Solver {
 #pragma unroll
             for (int j = 0; j < N; ++j) {
                 if (!nz(k, j)) continue;
-                gth[j] += G[k][j] * r[k];          // r holds h here
+                gth[j] += gx(k, j) * r[k];          // r holds h here
 #pragma unroll
                 for (int c = j; c < N; ++c)
-                    if (nz(k, c)) H[j][c] += G[k][j] * G[k][c];
+                    if (nz(k, c)) H[j][c] += gx(k, j) * gx(k, c);
             }
         }
         if constexpr (BALL) {                      // the ball rows' products, zeros dropped
@@ -1205,7 +1266,7 @@ struct Solver {
 #pragma unroll
                 for (int e = 0; e < 3; ++e) {
                     const int k = OR + SD * b + e;
-                    double g[4] = {cq[b][e][0], cq[b][e][1], cq[b][e][2], (e == 0) ? cc0[b] : 0.0};
+                    double g[4] = {cqx(b, e, 0), cqx(b, e, 1), cqx(b, e, 2), (e == 0) ? ccx(b) : 0.0};
 #pragma unroll
                     for (int j = 0; j < N; ++j) {
                         if (j == 3 && e != 0) continue;
@@ -1325,6 +1386,7 @@ struct Solver {
                 }
             }
 #endif
+            grefresh();
             // ---- NT scalings, residuals, normal matrix (pdip.py:410-434)
             SocState so[SSA];
             double Hm[N][N];
@@ -1339,12 +1401,12 @@ struct Solver {
                 double g[N];
 #pragma unroll
                 for (int j = 0; j < N; ++j)
-                    if (nz(k, j)) g[j] = G[k][j] * d;
+                    if (nz(k, j)) g[j] = gx(k, j) * d;
 #pragma unroll
                 for (int j = 0; j < N; ++j)
 #pragma unroll
                     for (int c = j; c < N; ++c)
-                        if (nz(k, j) && nz(k, c)) Hm[j][c] += g[j] * G[k][c];
+                        if (nz(k, j) && nz(k, c)) Hm[j][c] += g[j] * gx(k, c);
             }
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
@@ -1375,6 +1437,7 @@ struct Solver {
             double dsS[SSA * SD], dzS[SSA * SD];         // SOC rows of the affine step
             double dx[N];
             double cmax = 1.0, p1 = 0.0, p2 = 0.0;
+            grefresh();
             predictor<FULL>(so, isz, F, idg, dx, cp, dsS, dzS, cmax, p1, p2);
             soc_bound(so, dsS, dzS, cmax);
             const double aa = frcp1(R::max(cmax));                   // quirk Q5 (no 0.99)
@@ -1407,8 +1470,10 @@ struct Solver {
             const double smu = sigma * mu;
             double sbzt[SSA][SD], slds[SSA][SD];
             DCOL_ISTAMP(it, 4);
+            grefresh();
             rhs_solve(so, isz, F, idg, cp, smu, dx, sbzt, slds);
             DCOL_ISTAMP(it, 5);
+            grefresh();
             cmax = 1.0;
             double cu[OR > 0 ? OR : 1], cdz[OR > 0 ? OR : 1];   // G dx and dz, kept for the update
 #pragma unroll
@@ -1476,7 +1541,7 @@ struct Solver {
             const double t = !cp ? -((z[k] * ilv(k, isz)) * (s[k] + r[k])) : -orth_num(k, cp, smu, s[k] + r[k]) * ilv(k, isz);
 #pragma unroll
             for (int j = 0; j < N; ++j)
-                if (nz(k, j)) rhs[j] += G[k][j] * t;
+                if (nz(k, j)) rhs[j] += gx(k, j) * t;
         }
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
@@ -1546,6 +1611,7 @@ struct Solver {
                            double& p1, double& p2) const {
         double sbzt[SSA][SD], slds[SSA][SD];
         rhs_solve(so, isz, F, idg, nullptr, 0.0, dx, sbzt, slds);
+        grefresh();
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
             const double u = rowdot(k, dx);
@@ -1691,7 +1757,7 @@ struct Solver {
             if (PART && k >= PL) continue;   // extra-column rows: G[k][0:3] = 0
             const double zk = owns_row(k, prim) ? (wt ? wt[k] : z[k]) : 0.0;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) g.u[c] = fma(zk, G[k][c], g.u[c]);
+            for (int c = 0; c < 3; ++c) g.u[c] = fma(zk, gx(k, c), g.u[c]);
         }
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
@@ -1703,12 +1769,12 @@ struct Solver {
                 if constexpr (CONE) {
                     if (e < 3) {                                          // cone rows: Qe(-E e_k)
 #pragma unroll
-                        for (int c = 0; c < 3; ++c) g.u[c] = fma(ze, cq[b][e][c], g.u[c]);
+                        for (int c = 0; c < 3; ++c) g.u[c] = fma(ze, cqx(b, e, c), g.u[c]);
                     }
                 } else if constexpr (!BALL) {
                     const double zc = (g.kind == SOC_CONE) ? ze : 0.0;   // cone rows: Qe(-E e_k)
 #pragma unroll
-                    for (int c = 0; c < 3; ++c) g.u[c] = fma(zc, G[OR + SD * b + e][c], g.u[c]);
+                    for (int c = 0; c < 3; ++c) g.u[c] = fma(zc, gx(OR + SD * b + e, c), g.u[c]);
                 }
             }
         }
@@ -1891,12 +1957,12 @@ struct Solver {
             double g[N];
 #pragma unroll
             for (int j = 0; j < N; ++j)
-                if (nz(k, j)) g[j] = G[k][j] * dd[k];
+                if (nz(k, j)) g[j] = gx(k, j) * dd[k];
 #pragma unroll
             for (int j = 0; j < N; ++j)
 #pragma unroll
                 for (int c = j; c < N; ++c)
-                    if (nz(k, j) && nz(k, c)) Hm[j][c] += g[j] * G[k][c];
+                    if (nz(k, j) && nz(k, c)) Hm[j][c] += g[j] * gx(k, c);
         }
         SocNT W[SSA];
 #pragma unroll
@@ -1971,6 +2037,10 @@ struct Solver {
 // ------------------------------------------------------------------------------------
 // kernel
 // ------------------------------------------------------------------------------------
+#ifndef DCOL_BLOCK
+#define DCOL_BLOCK 64
+#endif
+constexpr int kLdsLanes = DCOL_BLOCK;   // GLDS: lanes per workgroup sharing the LDS row array
 // Hide a pointer's provenance from the optimiser (forces fresh loads through it).
 template <typename P>
 DCOL_HD void launder(P& p) {
@@ -1986,8 +2056,9 @@ DCOL_HD void launder(P& p) {
 // (dcol_capi.cpp: bucket_pairs).
 // MODE 0: one launch; 1: main launch of a suspend / resume pair (KArgs susp_*); 2: the
 // resume launch, for continuation entry ci (pi = its pair)
+// GLDS: G rows in LDS (Solver; the one-wave-per-workgroup solve kernels only)
 template <int N, int NSOC, int OMAX, int LPP, bool FULL = false, bool BALL = false, bool CONE = false, int OE = 0,
-          int MODE = 0>
+          int MODE = 0, bool GLDS = false>
 DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1, int k1o = -1, int k2o = -1) {
     DCOL_STAMP(A, pi, q, 0);
     const int64_t B = A.B;
@@ -2009,9 +2080,16 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1, int k
     make_frame(S2, th2, F2, plain2);
     DCOL_STAMP(A, pi, q, 1);
 
-    using Slv = Solver<N, NSOC, OMAX, LPP, BALL, CONE, OE>;
+    using Slv = Solver<N, NSOC, OMAX, LPP, BALL, CONE, OE, GLDS>;
     Slv P;
     P.q = q;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (GLDS) {
+        static_assert(kLdsLanes == 64, "GLDS: one wave per workgroup");
+        __shared__ double rows_lds[Slv::LDSW * 64];
+        P.gb = (typename Slv::lds_d*)&rows_lds[threadIdx.x & 63];
+    }
+#endif
 #ifdef DCOL_STAMPS
     P.dbg = (q == 0) ? A.stamps + 16 * pi + 8 : nullptr;
 #endif
@@ -2163,20 +2241,28 @@ static_assert(kSolveBlock % 64 == 0, "one or more whole waves per workgroup");
 // FL: variant flags, bit 0 FULL, bit 1 BALL, bit 2 CONE (variants.py)
 // OE > 0: the row-partitioned (PART) copy with OE extra-column row slots (Solver).
 // FL bit 4 (16): the main launch of a suspend / resume pair (solve_one MODE 1)
+// WPS >= 10: the LDS-rows copy (Solver GLDS) at WPS - 10 waves per SIMD (variants.py);
+// DCOL_NO_GLDS builds every copy with register rows (the codegen-invariance twin, A/B)
+#ifdef DCOL_NO_GLDS
+constexpr bool kGlds = false;
+#else
+constexpr bool kGlds = true;
+#endif
 template <int N, int NSOC, int OMAX, int LPP, int WPS, int FL, int OE = 0>
-__global__ void __launch_bounds__(kSolveBlock, WPS) prox_kernel(KArgs A) {
+__global__ void __launch_bounds__(kSolveBlock, WPS % 10) prox_kernel(KArgs A) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t slot = t / LPP;
     const int q = (int)(t % LPP);
     if (slot >= A.n) return;
     const int64_t pi = A.perm ? (int64_t)A.perm[A.slot0 + slot] : (A.slot0 + slot);
-    solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0, OE, (FL & 16) ? 1 : 0>(A, pi, q);
+    solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0, OE, (FL & 16) ? 1 : 0,
+              kGlds && WPS >= 10>(A, pi, q);
 }
 
 // The resume launch of a suspend / resume pair: one lane group per continuation entry;
 // entries past the count the main launch appended exit at once.
 template <int N, int NSOC, int OMAX, int LPP, int WPS, int FL, int OE = 0>
-__global__ void __launch_bounds__(kSolveBlock, WPS) prox_resume_kernel(KArgs A) {
+__global__ void __launch_bounds__(kSolveBlock, WPS % 10) prox_resume_kernel(KArgs A) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t ci = t / LPP;
     const int q = (int)(t % LPP);

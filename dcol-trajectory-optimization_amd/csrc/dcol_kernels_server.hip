@@ -53,10 +53,15 @@ __global__ void __launch_bounds__(kSolveBlock, 1) prox_pair_server(KArgs Args, P
     box_st(&box->xcd, __builtin_amdgcn_s_getreg(6164) & 0xf);   // hwreg(HW_REG_XCC_ID, 0, 4)
     long long t0 = wall_clock64();
     for (;;) {
-        // one round trip per poll: the id word and the stop flag in flight with the request word
+        // one round trip per poll: the id word and the stop flag in flight with the request
+        // word.  All three RELAXED: a system-scope acquire load is followed by a cache
+        // invalidation (buffer_inv sc0 sc1), and one per poll -- every microsecond or so --
+        // kept invalidating the L2 under whatever else ran on the GPU: a 100k batch plan ran
+        // 1.6x slower beside a resident server (tests/test_dropin.py ..._does_not_tax_...).
+        // The acquire is one fence per request instead (below).
         uint64_t ids = box_ld64(&box->ids);
         const bool stop = box_ld(&box->stop) != 0;
-        const uint64_t r = box_ld64<__ATOMIC_ACQUIRE>(&box->req);
+        const uint64_t r = box_ld64(&box->req);
         const int32_t req = (int32_t)(r >> 32);
         if (req == last) {
             if (!stop && wall_clock64() - t0 < idle_ticks) {
@@ -72,6 +77,8 @@ __global__ void __launch_bounds__(kSolveBlock, 1) prox_pair_server(KArgs Args, P
             box_st(&box->alive, 1);
             continue;
         }
+        // a new request: acquire it (the poses and the id word were written before it)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         const long long w0 = wall_clock64(), c0 = clock64();
         if ((ids >> 48) != ((uint32_t)req & 0xffffu)) ids = box_ld64(&box->ids);   // read before this request's
         const int vid = (int)(r & 0xffffu);

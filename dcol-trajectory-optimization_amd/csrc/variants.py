@@ -107,7 +107,12 @@ CONFIG = {
 }
 # per-flavour overrides for the structured copies (FL 2 = BALL, 4 = CONE): their register
 # footprint differs from the dense kernel's, so their spill-free (LPP, WPS) can too
-CONFIG_FL = {}
+# WPS >= 10: the copy holds its G rows (and CONE rows) in LDS instead of registers
+# (dcol_device.hpp Solver GLDS) and runs WPS - 10 waves per SIMD.  The one-lane cone x box
+# kernel: 349 VGPRs at one wave -> 256 at two waves with 18 scratch instructions per loop
+# (tools/isa_stats.py 4:1:7:1:0:37 --waves 2), bitwise equal; cone x polytope 11.8 -> 12.2e8,
+# polytope x cone 11.8 -> 12.1e8 pair-solves/s (profiles/r05_b/cls_*.log, two rounds each).
+CONFIG_FL = {(4, 1, 7, 4): [(1, 12)]}
 FULL = {(4, 0)}   # shapes with padding-free copies (see module docstring)
 # padding-free copies of the structured-cone kernels: (N, NSOC, OMAX) whose pairs commonly
 # fill the bucket (cone x box: the cone's base row + 6 faces = 7)
@@ -160,6 +165,9 @@ def configs_fl(n, nsoc, omax, fl):
 PART = {
     # x polytope: one lane per pair (the SOC block would otherwise idle the group's other lane;
     # measured 200k pairs: capsule x box 8.1e8 at LPP 2 -> 9.5e8, cylinder x box 6.6 -> 7.1e8)
+    # (LDS rows at one wave per SIMD -- WPS 11, fewer values parked in AGPRs -- measured slower
+    # here: capsule x polytope -5 %, cylinder x polytope -10 %, polygon x polytope +-0
+    # (profiles/r05_b/cls_*.log); the register rows stay)
     (5, 1): {(8, 2): [(1, 1), (2, 1)], (10, 2): [(1, 1), (2, 1)], (14, 2): [(2, 1)], (18, 2): [(2, 1)]},
     # x sphere / cone: both lanes own a SOC block (capsule x sphere 11.2e8 at LPP 2, 9.1e8 at 1)
     # two waves per SIMD where the allocator then spills at most a few scratch accesses per

@@ -1,10 +1,11 @@
 """Child process of tests/test_dropin.py::test_pair_server_*_exit: makes drop-in calls so the
 one-pair server is resident (long idle time), then exits WITHOUT destroying anything.
 argv[1]: "python" -- the normal exit (the binding's atexit hook and the library's exit
-handler both run); "c" -- the binding's atexit hook unregistered, so only the library's own
-exit handler (registered at the first server start) stops the server; "reopen" -- a fresh
-process: create a table and solve pairs (the device must be usable after the others)."""
-import atexit
+handler both run); "c" -- the C library's exit() called directly, so Python's own teardown
+(atexit hooks, Table.__del__) never runs and only the library's exit handler (registered at
+the first server start) can stop the server, as in a C host that exits without destroying
+its tables; "reopen" -- a fresh process: create a table and solve pairs (the device must be
+usable after the others)."""
 import os
 import sys
 
@@ -16,7 +17,6 @@ import numpy as np  # noqa: E402
 
 def main():
     mode = sys.argv[1]
-    from dcol_amd import _lib
     from dcol_amd.engine import default_engine
     from primitives.misc_primitive_constructor import SphereMRP, create_rect_prism
     from proximity.proximity import proximity_mrp
@@ -33,9 +33,11 @@ def main():
     eng = default_engine()
     st = eng.pair_stats()
     running = eng.pair_server_running()
-    if mode == "c":
-        atexit.unregister(_lib._shutdown)
     print(f"CHILD_OK mode={mode} served={st['served']} running={int(running)} alpha0={alphas[0]!r}", flush=True)
+    if mode == "c":
+        import ctypes
+        sys.stderr.flush()
+        ctypes.CDLL(None).exit(0)      # C exit(): the C exit handlers run, Python's teardown does not
     if mode == "reopen":
         eng.stop_pair_server()
         assert not eng.pair_server_running()

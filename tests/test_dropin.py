@@ -360,10 +360,11 @@ def _child(mode, env_extra, timeout=240):
 def test_pair_server_stopped_at_process_exit(mode):
     """A process that makes drop-in calls and exits without destroying its tables while the
     one-pair server is resident (idle time 60 s): the server is stopped at exit -- by the
-    binding's atexit hook (dcol_amd/_lib.py) or, with that unregistered, by the library's
-    own exit handler (dcol_shutdown, registered at the first server start) -- so the process
-    neither tears its HIP context down under a polling wave nor waits out the idle time.
-    Then a fresh process opens the device, solves pairs and stops its own server."""
+    binding's atexit hook (dcol_amd/_lib.py) on a normal Python exit, or, when the process
+    leaves through C exit() with no Python teardown at all, by the library's own exit handler
+    (dcol_shutdown, registered at the first server start) -- so the process neither tears
+    its HIP context down under a polling wave nor waits out the idle time.  Then a fresh
+    process opens the device, solves pairs and stops its own server."""
     env = {"DCOL_PAIR_SERVER": "1", "DCOL_PAIR_SERVER_IDLE_US": "60000000", "DCOL_DEBUG_SHUTDOWN": "1"}
     p, took = _child(mode, env)
     assert p.returncode == 0, p.stdout + p.stderr
