@@ -865,7 +865,7 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup, 
             el = float(t[0])
         return el, marks
 
-    settle = clock_settle(launch, stream, dev, wd, args.settle_ms)
+    settle_info = clock_settle(launch, stream, dev, wd, args.settle_ms)
     elapsed, marks = run_steps([step], "serial")
     # the solve's share of each timed step (start -> solved) and the whole step, same run
     kernel_ms = float(np.median([a.elapsed_time(b) for a, b, _ in marks]))
@@ -950,7 +950,7 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup, 
                          "kernel_ms": ranks_stats[:, 4].tolist(), "plan_run_ms": ranks_stats[:, 5].tolist(),
                          "iters_mean": ranks_stats[:, 2].tolist(), "pairs": ranks_stats[:, 3].astype(int).tolist()}},
         "kernel_ms_max_rank": float(ranks_stats[:, 4].max()),
-        "settle": settle,
+        "settle": settle_info,
         "pipeline": {"streams": max(1, len(lanes)), "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                      "note": "solves round-robin on the streams, all-gathers on one collective stream (an overlap "
                              "rate, not value)",

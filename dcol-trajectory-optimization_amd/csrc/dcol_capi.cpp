@@ -100,6 +100,7 @@ int pair_server_idle_us() {
 std::mutex g_tables_mu;
 std::vector<dcol_table*> g_tables;
 std::atomic<bool> g_shutdown{false};   // set by dcol_shutdown: no new server starts
+std::atomic<int> g_server_tables{0};   // tables whose pair server was ever started
 std::once_flag g_exit_hook;
 // how long table destroy / shutdown / a restart wait for a server to leave (it leaves at its
 // next poll, i.e. after at most the solve in hand: microseconds)
@@ -178,6 +179,7 @@ struct dcol_table {
     bool server_launched = false;  // a server was launched at least once (destroy stops it)
     int64_t n_served = 0, n_launched = 0, n_starts = 0;   // dcol_table_pair_stats
     int32_t srv_mismatch = 0;      // consecutive calls whose flags / tol / max_iter differ from the server's
+    std::atomic<bool> stop_req{false};   // a batch launch asked the server to leave (yield_pair_servers)
     double srv_us = 0.0, srv_cycles = 0.0;
 };
 
@@ -247,6 +249,28 @@ bool stop_pair_server(dcol_table* t, int timeout_ms) {
     __atomic_store_n(&t->pair_host->stop, 0, __ATOMIC_SEQ_CST);
     __atomic_store_n(&t->pair_host->alive, 0, __ATOMIC_SEQ_CST);
     return true;
+}
+
+// A batch launch on `device` asks every resident pair server there to leave (it does after
+// the request in hand, at its next poll), without waiting: a kernel resident beside a batch
+// plan slowed the plan by 1.3-2x depending on the server stream's kind and the number of
+// hardware queues (tools/server_tax.py, profiles/r05_d/, r05_e/), so the latency path gives
+// way to the throughput path.  The table's next dcol_prox_pair drains it and starts a new
+// server (one launch, ~10 us).
+void yield_pair_servers(int device) {
+    if (g_server_tables.load(std::memory_order_acquire) == 0) return;
+    static const bool off = [] {   // DCOL_PAIR_SERVER_YIELD=0: the server stays (A/B: tools/server_tax.py)
+        const char* e = std::getenv("DCOL_PAIR_SERVER_YIELD");
+        return e && std::atoi(e) == 0;
+    }();
+    if (off) return;
+    std::lock_guard<std::mutex> lk(g_tables_mu);
+    for (dcol_table* t : g_tables) {
+        if (t->device != device || !t->pair_host) continue;
+        if (!__atomic_load_n(&t->pair_host->alive, __ATOMIC_ACQUIRE)) continue;
+        __atomic_store_n(&t->pair_host->stop, 1, __ATOMIC_SEQ_CST);
+        t->stop_req.store(true, std::memory_order_release);
+    }
 }
 
 hipError_t launch_variant(int N, int nsoc, int omax, int lpp, int flags, const KArgs& a, hipStream_t st, int oe = 0) {
@@ -342,6 +366,7 @@ int dcol_table_destroy(dcol_table* t) {
     {
         std::lock_guard<std::mutex> lk(g_tables_mu);
         g_tables.erase(std::remove(g_tables.begin(), g_tables.end(), t), g_tables.end());
+        if (t->server_launched) g_server_tables.fetch_sub(1, std::memory_order_acq_rel);
     }
     DeviceGuard g(t->device);
     // the server exits at its next poll; one that does not (a hung device) keeps the whole
@@ -841,8 +866,9 @@ namespace {
 // epilogues; then alpha / grad / iters / status may be NULL)
 int plan_run_rec(const dcol_plan* p, const double* pose1, const double* pose2, double tol, int32_t max_iter,
                  int32_t flags, double* alpha, double* contact, double* grad, int32_t* iters, int32_t* status,
-                 double* rec, void* stream) {
+                 double* rec, void* stream, bool yield = true) {
     if (!p) return fail(DCOL_ERR_ARG, "dcol_plan_run: NULL plan");
+    if (yield) yield_pair_servers(p->table->device);   // (the pair call's own launch path keeps it)
     if (p->B == 0) return DCOL_SUCCESS;
     if (!pose1 || !pose2 || (!alpha && !rec))
         return fail(DCOL_ERR_ARG, "dcol_plan_run: pose1, pose2 and alpha are required");
@@ -958,16 +984,33 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
         }
         if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&t->pair_dev), t->pair_host, 0);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&t->pair_stream, hipStreamNonBlocking);
-        // The server stream at the device's highest priority: HIP pools hardware queues per
-        // priority level (GPU_MAX_HW_QUEUES each), so the resident server gets a queue of its
-        // own instead of sharing one with the caller's or the side streams, whose kernels
-        // would otherwise wait behind it until it idles out
-        int prio_lo = 0, prio_hi = 0;
-        if (e == hipSuccess && hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) {
-            (void)hipGetLastError();
-            prio_hi = 0;
+        // The server stream: a CU-masked stream (mask = every CU), because HIP never pools a
+        // CU-masked stream into a shared hardware queue -- the resident server gets a queue of
+        // its own instead of sharing one (GPU_MAX_HW_QUEUES, 4 by default) with the caller's
+        // or the side streams, whose kernels would otherwise wait behind it until it idles
+        // out.  Not a high-priority stream: a resident kernel on a high-priority queue slowed
+        // a normal-priority 100k batch plan 1.7-1.8x whatever its poll rate, a normal or
+        // CU-masked one by nothing measurable (tools/server_tax.py, profiles/r05_d/).
+        // DCOL_PAIR_SERVER_STREAM=normal / high: those alternatives (A/B).
+        const char* sk = std::getenv("DCOL_PAIR_SERVER_STREAM");
+        if (e == hipSuccess && sk && (std::strcmp(sk, "normal") == 0 || std::strcmp(sk, "high") == 0)) {
+            int prio_lo = 0, prio_hi = 0;
+            if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) {
+                (void)hipGetLastError();
+                prio_lo = prio_hi = 0;
+            }
+            e = hipStreamCreateWithPriority(&t->server_stream, hipStreamNonBlocking,
+                                            std::strcmp(sk, "high") == 0 ? prio_hi : prio_lo);
+        } else if (e == hipSuccess) {
+            int cus = 0;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, t->device) != hipSuccess || cus <= 0) {
+                (void)hipGetLastError();
+                cus = 256;
+            }
+            std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+            for (int c = 0; c < cus; ++c) mask[c / 32] |= 1u << (c % 32);
+            e = hipExtStreamCreateWithCUMask(&t->server_stream, (uint32_t)mask.size(), mask.data());
         }
-        if (e == hipSuccess) e = hipStreamCreateWithPriority(&t->server_stream, hipStreamNonBlocking, prio_hi);
         int khz = 0;
         if (e == hipSuccess && hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, t->device) != hipSuccess) {
             (void)hipGetLastError();
@@ -1005,6 +1048,10 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
     }
     PairBox* h = t->pair_host;
     PairBox* d = t->pair_dev;
+    // a batch launch asked the server to leave: drain it (it left at its next poll) and clear
+    // the stop flag, so the server started below stays
+    if (t->stop_req.exchange(false, std::memory_order_acq_rel) && !stop_pair_server(t, kServerStopMs))
+        return fail(DCOL_ERR_HIP, "dcol_prox_pair: the pair server did not stop within 5 s");
     std::memcpy(h->pose1, pose1, 6 * sizeof(double));
     std::memcpy(h->pose2, pose2, 6 * sizeof(double));
     // SoA of one pair = the 6 values in order; the kernel reads / writes the mapped memory.
@@ -1073,9 +1120,11 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
             // a resident wave must not outlive the process's HIP context: stop every server
             // at exit (the handler runs before the HIP runtime's own, registered earlier)
             std::call_once(g_exit_hook, [] { std::atexit([] { (void)dcol_shutdown(); }); });
+            if (!t->server_launched) g_server_tables.fetch_add(1, std::memory_order_acq_rel);
             t->server_launched = true;
             ++t->n_starts;
-            return launch_pair_server(a, d, (int64_t)idle_us * t->wall_ticks_us, t->server_stream);
+            const char* ps = std::getenv("DCOL_PAIR_SERVER_POLL_SLEEP");
+            return launch_pair_server(a, d, (int64_t)idle_us * t->wall_ticks_us, ps ? std::atoi(ps) : 0, t->server_stream);
         };
         if (restart && !stop_pair_server(t, kServerStopMs))   // it leaves at its next poll, then start anew
             return fail(DCOL_ERR_HIP, "dcol_prox_pair: the pair server did not stop within 5 s");
@@ -1127,7 +1176,7 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
     // row-partitioned x polytope kernels 4-5 % of throughput; the server serves the latency
     // path now.)
     int rc = plan_run_rec(plan, d->pose1, d->pose2, tol, max_iter, flags & ~DCOL_CASE4, &d->alpha, d->contact,
-                          d->grad, &d->iters, &d->status, nullptr, t->pair_stream);
+                          d->grad, &d->iters, &d->status, nullptr, t->pair_stream, false);
     if (rc != DCOL_SUCCESS) return rc;
     ++t->n_launched;
     const hipError_t e = hipStreamSynchronize(t->pair_stream);

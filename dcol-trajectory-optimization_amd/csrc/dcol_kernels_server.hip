@@ -45,7 +45,8 @@ using KArgsK = const __attribute__((address_space(4))) KArgs;   // in the kernel
 
 // Args (first kernel argument, offset 0 of the kernel-argument segment): the table pointers,
 // the mailbox's one-pair arrays and the server's flags / tolerance / iteration cap.
-__global__ void __launch_bounds__(kSolveBlock, 1) prox_pair_server(KArgs Args, PairBox* box, int64_t idle_ticks) {
+__global__ void __launch_bounds__(kSolveBlock, 1) prox_pair_server(KArgs Args, PairBox* box, int64_t idle_ticks,
+                                                                   int32_t poll_sleep) {
     (void)Args;
     constexpr uint64_t kIdMask = (1ull << kPairBoxIdBits) - 1;
     int32_t last = box_ld(&box->done);
@@ -66,6 +67,7 @@ __global__ void __launch_bounds__(kSolveBlock, 1) prox_pair_server(KArgs Args, P
         if (req == last) {
             if (!stop && wall_clock64() - t0 < idle_ticks) {
                 __builtin_amdgcn_s_sleep(2);
+                for (int i = 0; i < poll_sleep; ++i) __builtin_amdgcn_s_sleep(127);   // (A/B knob)
                 continue;
             }
             // leaving: clear alive, then look at the request word once more -- a caller that
@@ -125,9 +127,10 @@ __global__ void __launch_bounds__(kSolveBlock, 1) prox_pair_server(KArgs Args, P
     }
 }
 
-hipError_t launch_pair_server(const KArgs& args, PairBox* box, int64_t idle_ticks, hipStream_t stream) {
+hipError_t launch_pair_server(const KArgs& args, PairBox* box, int64_t idle_ticks, int32_t poll_sleep,
+                              hipStream_t stream) {
     if (!box || idle_ticks <= 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(prox_pair_server, dim3(1), dim3(kSolveBlock), 0, stream, args, box, idle_ticks);
+    hipLaunchKernelGGL(prox_pair_server, dim3(1), dim3(kSolveBlock), 0, stream, args, box, idle_ticks, poll_sleep);
     return hipGetLastError();
 }
 

@@ -63,7 +63,9 @@ constexpr int kPairBoxIdBits = 24;
 // a server on `stream` serving box (device view) with args' table pointers, flags, tolerance
 // and iteration cap; it exits after idle_ticks of the device wall clock
 // (hipDeviceAttributeWallClockRate) without a request
-hipError_t launch_pair_server(const KArgs& args, PairBox* box, int64_t idle_ticks, hipStream_t stream);
+// (poll_sleep: extra s_sleep(127) rounds between polls, DCOL_PAIR_SERVER_POLL_SLEEP; A/B)
+hipError_t launch_pair_server(const KArgs& args, PairBox* box, int64_t idle_ticks, int32_t poll_sleep,
+                              hipStream_t stream);
 #ifdef DCOL_CHECK_EXEC
 // diagnostic build: host reader of a translation unit's DPP-source violation counter
 // (dcol_device.hpp dpp_check), summed by dcol_debug_exec_violations (dcol_capi.cpp)

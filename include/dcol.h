@@ -198,8 +198,8 @@ int dcol_prox_batch_host(const dcol_table* table, int64_t B, const int32_t* shap
  * resident workgroup polling that memory, started by the first such call and leaving after
  * DCOL_PAIR_SERVER_IDLE_US (default 1000) without a request -- no kernel launch per call.
  * (A device-wide synchronisation issued meanwhile waits for it to leave.  The server runs
- * on a stream of the device's highest priority, so it holds a hardware queue of its own and
- * no kernel of another stream queues behind it.)  Other pairs,
+ * on a CU-masked stream, which HIP gives a hardware queue of its own, so no kernel of
+ * another stream queues behind it.)  Other pairs,
  * and every pair under DCOL_PAIR_SERVER=0, take one launch on a stream of the table.
  * Calls on one table are serialised.                                                      */
 int dcol_prox_pair(const dcol_table* table, int32_t shape1, int32_t shape2, const double* pose1,

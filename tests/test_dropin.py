@@ -382,12 +382,13 @@ def test_pair_server_stopped_at_process_exit(mode):
 
 
 @pytest.mark.gpu
-def test_pair_server_does_not_tax_batch_plan(engine, monkeypatch):
-    """A batch plan (100k poly x poly pairs, bench configs[3]) run while the one-pair server
-    is resident takes the same time as with it stopped (the server has its own
-    highest-priority hardware queue and one CU), and returns bitwise the same results; the
-    drop-in's launch path (a call with other flags) while the server is resident as well.
-    The measured figures are printed (tools/server_tax.py records them)."""
+def test_pair_server_gives_way_to_batch_plans(engine, monkeypatch):
+    """A batch plan launched while the one-pair server is resident makes it leave (a kernel
+    resident beside a batch plan slowed it 1.3-2x, tools/server_tax.py): the plan (100k poly x
+    poly pairs, bench configs[3]) then takes the time it takes with the server stopped, its
+    results are bitwise the same, the server has left after the launch and the next drop-in
+    call starts a new one and answers bitwise as before.  The drop-in's own launch path (a
+    call with other flags) does not make its server leave."""
     import torch
     from bench import pairs, shape_table
     from dcol_amd import alloc_outputs, spec_from_arrays
@@ -400,7 +401,7 @@ def test_pair_server_does_not_tax_batch_plan(engine, monkeypatch):
     ball = SphereMRP(0.4)
     box.r, box.p = np.zeros(3), np.array([0.1, -0.2, 0.3])
     ball.r, ball.p = np.array([2.0, 0.5, -0.3]), np.zeros(3)
-    engine.solve_pair(ball, box, grad=None)           # registers both: the table is final now
+    ref_pair = engine.solve_pair(ball, box, grad=None)   # registers both: the table is final now
     B = 100_000
     s1, s2, p1, p2 = pairs(B, len(tab["type"]), seed=3)
     plan = engine.plan(ids[s1], ids[s2], cache=False)
@@ -429,32 +430,19 @@ def test_pair_server_does_not_tax_batch_plan(engine, monkeypatch):
         engine.stop_pair_server()
         assert not engine.pair_server_running()
         t["stopped"].append(timed())
-        engine.solve_pair(ball, box, grad=None)       # the server is resident (30 s idle)
-        assert engine.pair_server_running()
+        np.testing.assert_array_equal(_bits([engine.solve_pair(ball, box, grad=None)]), _bits([ref_pair]))
+        assert engine.pair_server_running()           # resident (30 s idle) when the plans start
         t["resident"].append(timed())
-        assert engine.pair_server_running()
+        assert not engine.pair_server_running()       # it left at the first launch
         for k, v in out.items():
             assert torch.equal(v, ref[k]), k
-    # the launch path while the server is resident: a call with other flags
-    lat = {}
-    import time
-    for state in ("resident", "stopped"):
-        if state == "stopped":
-            monkeypatch.setenv("DCOL_PAIR_SERVER", "0")
-            engine.stop_pair_server()
-        else:
-            engine.solve_pair(ball, box, grad=None)
-        ts = []
-        for _ in range(50):
-            t0 = time.perf_counter()
-            engine.solve_pair(ball, box, grad="envelope")    # mismatching flags: launched
-            ts.append(time.perf_counter() - t0)
-            if state == "resident":
-                engine.solve_pair(ball, box, grad=None)      # (served: keeps the server's flags)
-        lat[state] = 1e6 * float(np.median(ts))
+    # the launch path (other flags) keeps the server
+    np.testing.assert_array_equal(_bits([engine.solve_pair(ball, box, grad=None)]), _bits([ref_pair]))
+    assert engine.pair_server_running()
+    engine.solve_pair(ball, box, grad="envelope")     # mismatching flags: launched, server stays
+    assert engine.pair_server_running()
     engine.stop_pair_server()
     stopped, resident = min(t["stopped"]), min(t["resident"])
-    print(f"server_tax: batch ms stopped {t['stopped']} resident {t['resident']} ratio {resident / stopped:.4f}; "
-          f"launch-path us resident {lat['resident']:.1f} stopped {lat['stopped']:.1f}")
-    assert resident / stopped < 1.10, t
-    assert lat["resident"] < 3 * lat["stopped"] + 50, lat
+    print(f"server_yield: batch ms stopped {t['stopped']} server resident at launch {t['resident']} "
+          f"ratio {resident / stopped:.4f}")
+    assert resident / stopped < 1.05, t
