@@ -197,7 +197,8 @@ struct Launch {
     bool full = false;   // every pair has o == omax: the padding-free kernel (DCOL_FULL_VARIANTS) if built
     bool ball = false;   // every SOC block is a ball block: the structured kernel (DCOL_BALL_VARIANTS) if built
     bool cone = false;   // every SOC block is a cone block (N = 4): DCOL_CONE_VARIANTS if built
-    int flags() const { return (full ? LF_FULL : 0) | (ball ? LF_BALL : 0) | (cone ? LF_CONE : 0); }
+    bool box = false;    // every pair is box x box (DevShape::boxp; with full): DCOL_BOX_VARIANTS if built
+    int flags() const { return (full ? LF_FULL : 0) | (ball ? LF_BALL : 0) | (cone ? LF_CONE : 0) | (box ? LF_BOX : 0); }
     int32_t code;   // reject status
     int64_t slot0, n;
     int lane = 0;   // 0 = caller's stream, 1..kSideStreams = table side stream
@@ -417,6 +418,12 @@ bool ball_disabled() {
     static const bool off = std::getenv("DCOL_NO_BALL") != nullptr;
     return off;
 }
+// DCOL_NO_BOX=1: box x box pairs run the padding-free dense-row kernel (A/B runs, tests)
+bool box_disabled() {
+    static const bool off = std::getenv("DCOL_NO_BOX") != nullptr;
+    return off;
+}
+
 // DCOL_NO_CONE=1: cone-SOC pairs run the dense (padded) kernels (A/B runs, tests)
 bool cone_disabled() {
     static const bool off = std::getenv("DCOL_NO_CONE") != nullptr;
@@ -488,7 +495,8 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
             c = classify(a, b, case4, false);
         if (lat_part && c.status == DCOL_OK && c.oe > 0 && part_lpp(c.N, c.nsoc, c.omax, c.oe, true) < 2)
             c = classify(a, b, case4, false);
-        const int ball = c.nsoc == 0 ? 0
+        // (3: box x box in the 12-row bucket -- the BOX kernels' axis-pair rows; nsoc == 0)
+        const int ball = c.nsoc == 0 ? ((a.boxp && b.boxp && c.N == 4 && c.omax == 12 && c.o == 12 && !box_disabled()) ? 3 : 0)
                          : (none_cone && !ball_disabled()) ? 1
                          : (all_cone && c.N == 4 && !cone_disabled()) ? 2 : 0;
         // a row-partitioned bucket only where its SOC flavour is compiled: the x polytope
@@ -497,7 +505,7 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
         if (c.status == DCOL_OK && c.oe > 0 && !part_flavour_built(c.N, c.nsoc, c.omax, c.oe, c.lpp, ball == 1))
             c = classify(a, b, case4, false);
         // flavour's own list (row-partitioned buckets have theirs: PairClass::lpp)
-        if (c.status == DCOL_OK && ball && c.oe == 0) c.lpp = choose_lpp(c.N, c.nsoc, c.omax, 2 * ball);
+        if (c.status == DCOL_OK && (ball == 1 || ball == 2) && c.oe == 0) c.lpp = choose_lpp(c.N, c.nsoc, c.omax, 2 * ball);
         Key k = c.status == DCOL_OK ? Key{0, c.N, c.nsoc, c.omax, c.lpp, ball, 0, c.oe} : Key{1, 0, 0, 0, 0, 0, c.status, 0};
         auto it = gid_of_key.emplace(k, (int32_t)groups.size()).first;
         if (it->second == (int32_t)groups.size()) groups.push_back(Group{k});
@@ -558,6 +566,7 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
         L.full = L.kind == 0 && G.full;
         L.ball = L.kind == 0 && std::get<5>(G.key) == 1;
         L.cone = L.kind == 0 && std::get<5>(G.key) == 2;
+        L.box = L.kind == 0 && std::get<5>(G.key) == 3 && L.full;
         L.slot0 = at;
         L.n = G.n;
         if (L.kind == 0 && !lpp_forced() && L.n * L.lpp < 64LL * t->simds && (small_plan || per_launch))

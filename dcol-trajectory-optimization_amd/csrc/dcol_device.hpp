@@ -111,7 +111,8 @@ struct DevShape {
                        // cylinder caps); the other n_ort - n_p rows have the extra-column form
                        // [0 0 0, g3, ex] (capsule / cylinder segment rows, polygon edges).  In the
                        // row pool the extra-column rows come first, then the pose rows.
-    int32_t pad2;
+    int32_t boxp;      // polytope of 6 rows whose rows 3..5 are the exact negatives of rows 0..2
+                       // (rect prisms: create_rect_prism) -- the BOX kernels (Solver)
     double R;          // ball SOC radius (sphere/capsule/cylinder/polygon)
     double cone_c;     // cone SOC row 0, column 3: -(tan(beta) * 3 * H / 4)
     double tanb;       // cone: tan(beta)  (E = diag(tanb, 1, 1))
@@ -637,12 +638,23 @@ struct Grp<4> {
 // 4 or 3 instead of 6, and it holds 4 or 3 doubles of G instead of 6.  The rows' reference
 // order within a pair changes, i.e. the lane sums add the same terms in another order
 // (rounding level); parity is pinned by iteration-count equality on every golden vector.
-template <int N, int NSOC, int OMAX, int LPP, bool BALL = false, bool CONE = false, int OE = 0, bool GLDS = false>
+template <int N, int NSOC, int OMAX, int LPP, bool BALL = false, bool CONE = false, int OE = 0, bool GLDS = false,
+          bool BOX = false>
 struct Solver {
     static_assert(OMAX % LPP == 0, "OMAX must be a multiple of LPP");
     static_assert(!(BALL && CONE) && (!CONE || N == 4), "CONE: cone-only SOC blocks of N = 4 pairs");
     static_assert(OE % LPP == 0 && OE <= OMAX && (OE == 0 || (N == 5 || N == 6)), "PART: N = 5 / 6, OE % LPP == 0");
     static constexpr bool PART = OE > 0;
+    // BOX: both primitives are boxes (DevShape::boxp) and every slot holds a row (FULL).  A
+    // lane's slots hold whole AXIS PAIRS: slots 2m, 2m + 1 = rows a, a + 3 of one primitive,
+    // G = [u, g3] and [-u, g3'] with u = Qe a_a, so the pair's products share u: the normal
+    // matrix takes (d + d') u u' + (d g3 - d' g3') u + (d g3^2 + d' g3'^2) e3 e3' instead of two
+    // rank-one updates, G'v takes (t - t') u, a row product u.v is formed once for both rows,
+    // and -u is never stored.  Axis pair t = m * LPP + q: t < 3 primitive 1's axis t, else
+    // primitive 2's axis t - 3.  The reassociated sums are rounding-level (parity: iteration
+    // counts and values against the oracle on every golden and every pair of the 100k set).
+    static_assert(!BOX || (N == 4 && NSOC == 0 && !PART && (OMAX / LPP) % 2 == 0 && OMAX == 12),
+                  "BOX: box x box pairs, whole axis pairs per lane");
     static constexpr int OR = OMAX / LPP;              // orthant slots per lane
     static constexpr int EL = OE / LPP;                // PART: extra-column slots per lane (the last EL)
     static constexpr int PL = OR - EL;                 // PART: pose slots per lane (the first PL)
@@ -714,6 +726,22 @@ struct Solver {
         if constexpr (GLDS) asm volatile("" : "+v"(gb));
 #endif
     }
+    // G entry (k, j) by value: BOX slot 2m + 1 holds only column 3 (its columns 0..2 are the
+    // exact negatives of slot 2m's)
+    DCOL_HD double gr(int k, int j) const {
+        if constexpr (BOX) {
+            if ((k & 1) && j < 3) return -static_cast<double>(gx(k - 1, j));
+        }
+        return gx(k, j);
+    }
+    // BOX: u.v of axis pair m (the same expression for both rows: one evaluation after CSE)
+    DCOL_HD double qdot(int m, const double* v) const {
+        double acc = gr(2 * m, 0) * v[0];
+        acc += gr(2 * m, 1) * v[1];
+        acc += gr(2 * m, 2) * v[2];
+        return acc;
+    }
+    DCOL_HD int box_prim(int m) const { return m * LPP + q >= 3 ? 1 : 0; }   // BOX: primitive of axis pair m
     double s[M], z[M], r[M];   // slack, dual, primal residual G x - h
     double x[N];
     double vimp[N];            // implicit-gradient mode: H^-1 e3 at the returned iterate
@@ -806,6 +834,24 @@ struct Solver {
             for (int k = PL; k < OR; ++k) {
                 const int i = (k - PL) * LPP + q;
                 ext_row(rows, k, i < oe, eb + i);
+            }
+        } else if constexpr (BOX) {
+            // axis pair m of this lane: rows a, a + 3 of one primitive (see BOX above); the
+            // second row's u and h are the exact negatives of the first's, only its g3 is loaded
+#pragma unroll
+            for (int m = 0; m < OR / 2; ++m) {
+                const int t = m * LPP + q;
+                const bool p2 = t >= 3;
+                const int a = p2 ? t - 3 : t;
+                Frame F;
+#pragma unroll
+                for (int c = 0; c < 9; ++c) F.Qe[c] = p2 ? F2.Qe[c] : F1.Qe[c];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) F.re[c] = p2 ? F2.re[c] : F1.re[c];
+                const int ri = (p2 ? S2.row_off : S1.row_off) + a;
+                orth_row(rows, 2 * m, true, p2, ri, F);
+                gx(2 * m + 1, 3) = rows[8 * (int64_t)(ri + 3) + 3];   // DevRow g3
+                r[2 * m + 1] = -r[2 * m];
             }
         } else {
 #pragma unroll
@@ -928,6 +974,11 @@ struct Solver {
 
     // -------- small dense helpers ------------------------------------------------------
     DCOL_HD double rowdot(int k, const double* v) const {
+        if constexpr (BOX)
+            if (k < OR) {   // u.v shared by the pair's two rows (CSE)
+                const double uv = qdot(k / 2, v);
+                return fma(gr(k, 3), v[3], (k & 1) ? -uv : uv);
+            }
         if constexpr (BALL)
             if (k >= OR) return ball_row(k, v);
         if constexpr (CONE)
@@ -935,14 +986,14 @@ struct Solver {
         if constexpr (PART)
             if (k < OR) {   // the slot's structural nonzeros only
                 const int j0 = k < PL ? 0 : 3, j1 = k < PL ? 4 : N;
-                double acc = gx(k, j0) * v[j0];
+                double acc = gr(k, j0) * v[j0];
 #pragma unroll
-                for (int j = j0 + 1; j < j1; ++j) acc += gx(k, j) * v[j];
+                for (int j = j0 + 1; j < j1; ++j) acc += gr(k, j) * v[j];
                 return acc;
             }
-        double acc = gx(k, 0) * v[0];
+        double acc = gr(k, 0) * v[0];
 #pragma unroll
-        for (int j = 1; j < N; ++j) acc += gx(k, j) * v[j];
+        for (int j = 1; j < N; ++j) acc += gr(k, j) * v[j];
         return acc;
     }
     // BALL: row e of SOC slot b times v
@@ -987,7 +1038,7 @@ struct Solver {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
-                for (int j = 0; j < N; ++j) out[j] += gx(k0 + e, j) * v[e];
+                for (int j = 0; j < N; ++j) out[j] += gr(k0 + e, j) * v[e];
         }
     }
     // gt = W^-1 G_b (SD x N), the SOC block of G~ (NT_scaling.py:164-202)
@@ -1029,7 +1080,7 @@ struct Solver {
             for (int j = 0; j < N; ++j) {
                 double col[4], res[4];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) col[e] = gx(k0 + e, j);
+                for (int e = 0; e < 4; ++e) col[e] = gr(k0 + e, j);
                 soc_solve(W, col, res);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) gt[e][j] = res[e];
@@ -1229,16 +1280,37 @@ struct Solver {
 #pragma unroll
             for (int c = j; c < N; ++c) H[j][c] = 0.0;
         }
+        if constexpr (BOX) {                       // axis pairs: G'G = 2 u u' + ..., G'h = (h - h') u + ...
+#pragma unroll
+            for (int m = 0; m < OR / 2; ++m) {
+                const int k = 2 * m;
+                const double ge = gr(k, 3), go = gr(k + 1, 3);
+                const double dh = r[k] - r[k + 1];
+                const double cg = ge - go;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const double uj = gr(k, j);
+                    gth[j] = fma(uj, dh, gth[j]);
+                    const double u2 = 2.0 * uj;
+#pragma unroll
+                    for (int c = j; c < 3; ++c) H[j][c] = fma(u2, gr(k, c), H[j][c]);
+                    H[j][3] = fma(uj, cg, H[j][3]);
+                }
+                gth[3] = fma(ge, r[k], fma(go, r[k + 1], gth[3]));
+                H[3][3] = fma(ge, ge, fma(go, go, H[3][3]));
+            }
+        } else {
 #pragma unroll
         for (int k = 0; k < MG; ++k) {
 #pragma unroll
             for (int j = 0; j < N; ++j) {
                 if (!nz(k, j)) continue;
-                gth[j] += gx(k, j) * r[k];          // r holds h here
+                gth[j] += gr(k, j) * r[k];          // r holds h here
 #pragma unroll
                 for (int c = j; c < N; ++c)
-                    if (nz(k, c)) H[j][c] += gx(k, j) * gx(k, c);
+                    if (nz(k, c)) H[j][c] += gr(k, j) * gr(k, c);
             }
+        }
         }
         if constexpr (BALL) {                      // the ball rows' products, zeros dropped
 #pragma unroll
@@ -1394,6 +1466,27 @@ struct Solver {
             for (int j = 0; j < N; ++j)
 #pragma unroll
                 for (int c = j; c < N; ++c) Hm[j][c] = 0.0;
+            if constexpr (BOX) {
+                // axis pair (rows [u, ge], [-u, go], W^-2 = d, d'): (d + d') u u' in the 3 x 3
+                // block, (d ge - d' go) u in column 3, d ge^2 + d' go^2 at (3, 3)
+#pragma unroll
+                for (int m = 0; m < OR / 2; ++m) {
+                    const int k = 2 * m;
+                    const double de = z[k] * ilv(k, isz), dO = z[k + 1] * ilv(k + 1, isz);
+                    const double ge = gr(k, 3), go = gr(k + 1, 3);
+                    const double ue = de * ge, uo = dO * go;
+                    const double sd = de + dO, cg = ue - uo;
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) {
+                        const double uj = gr(k, j);
+                        const double su = sd * uj;
+#pragma unroll
+                        for (int c = j; c < 3; ++c) Hm[j][c] = fma(su, gr(k, c), Hm[j][c]);
+                        Hm[j][3] = fma(cg, uj, Hm[j][3]);
+                    }
+                    Hm[3][3] = fma(ue, ge, fma(uo, go, Hm[3][3]));
+                }
+            } else {
 #pragma unroll
             for (int k = 0; k < OR; ++k) {
                 const double zk = z[k];
@@ -1401,12 +1494,13 @@ struct Solver {
                 double g[N];
 #pragma unroll
                 for (int j = 0; j < N; ++j)
-                    if (nz(k, j)) g[j] = gx(k, j) * d;
+                    if (nz(k, j)) g[j] = gr(k, j) * d;
 #pragma unroll
                 for (int j = 0; j < N; ++j)
 #pragma unroll
                     for (int c = j; c < N; ++c)
-                        if (nz(k, j) && nz(k, c)) Hm[j][c] += g[j] * gx(k, c);
+                        if (nz(k, j) && nz(k, c)) Hm[j][c] += g[j] * gr(k, c);
+            }
             }
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
@@ -1534,14 +1628,29 @@ struct Solver {
         double rhs[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) rhs[j] = 0.0;
-#pragma unroll
-        for (int k = 0; k < OR; ++k) {
+        const auto tk = [&](int k) {
             // (W^-1 b~z)_k - z_k; the predictor's -(z (s + r)) / s reuses W^-2 = z / s of the
             // normal matrix (dd)
-            const double t = !cp ? -((z[k] * ilv(k, isz)) * (s[k] + r[k])) : -orth_num(k, cp, smu, s[k] + r[k]) * ilv(k, isz);
+            return !cp ? -((z[k] * ilv(k, isz)) * (s[k] + r[k])) : -orth_num(k, cp, smu, s[k] + r[k]) * ilv(k, isz);
+        };
+        if constexpr (BOX) {   // axis pair: (t - t') u, ge t + go t'
+#pragma unroll
+            for (int m = 0; m < OR / 2; ++m) {
+                const int k = 2 * m;
+                const double te = tk(k), to = tk(k + 1);
+                const double dt = te - to;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) rhs[j] = fma(gr(k, j), dt, rhs[j]);
+                rhs[3] = fma(gr(k, 3), te, fma(gr(k + 1, 3), to, rhs[3]));
+            }
+        } else {
+#pragma unroll
+        for (int k = 0; k < OR; ++k) {
+            const double t = tk(k);
 #pragma unroll
             for (int j = 0; j < N; ++j)
-                if (nz(k, j)) rhs[j] += gx(k, j) * t;
+                if (nz(k, j)) rhs[j] += gr(k, j) * t;
+        }
         }
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
@@ -1723,6 +1832,7 @@ struct Solver {
     // orthant slot k holds a row of primitive prim that enters the pose aggregate (PART: the
     // pose slots; the extra-column rows have no pose columns)
     DCOL_HD bool owns_row(int k, int prim) const {
+        if constexpr (BOX) return box_prim(k / 2) == prim;
         if constexpr (PART) {
             if (k >= PL) return false;
             const int i = k * LPP + q;
@@ -1752,12 +1862,22 @@ struct Solver {
         g.u[0] = g.u[1] = g.u[2] = 0.0;
         g.zs[0] = g.zs[1] = g.zs[2] = g.zs[3] = 0.0;
         g.kind = NSOC > 0 ? S.soc_kind : SOC_NONE;   // polytope pairs: no record read
+        if constexpr (BOX) {   // axis pair: (z - z') u
+#pragma unroll
+            for (int m = 0; m < OR / 2; ++m) {
+                const int k = 2 * m;
+                const double zd = owns_row(k, prim) ? (wt ? wt[k] - wt[k + 1] : z[k] - z[k + 1]) : 0.0;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) g.u[c] = fma(zd, gr(k, c), g.u[c]);
+            }
+        } else {
 #pragma unroll
         for (int k = 0; k < OR; ++k) {
             if (PART && k >= PL) continue;   // extra-column rows: G[k][0:3] = 0
             const double zk = owns_row(k, prim) ? (wt ? wt[k] : z[k]) : 0.0;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) g.u[c] = fma(zk, gx(k, c), g.u[c]);
+            for (int c = 0; c < 3; ++c) g.u[c] = fma(zk, gr(k, c), g.u[c]);
+        }
         }
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
@@ -1774,7 +1894,7 @@ struct Solver {
                 } else if constexpr (!BALL) {
                     const double zc = (g.kind == SOC_CONE) ? ze : 0.0;   // cone rows: Qe(-E e_k)
 #pragma unroll
-                    for (int c = 0; c < 3; ++c) g.u[c] = fma(zc, gx(OR + SD * b + e, c), g.u[c]);
+                    for (int c = 0; c < 3; ++c) g.u[c] = fma(zc, gr(OR + SD * b + e, c), g.u[c]);
                 }
             }
         }
@@ -1957,12 +2077,12 @@ struct Solver {
             double g[N];
 #pragma unroll
             for (int j = 0; j < N; ++j)
-                if (nz(k, j)) g[j] = gx(k, j) * dd[k];
+                if (nz(k, j)) g[j] = gr(k, j) * dd[k];
 #pragma unroll
             for (int j = 0; j < N; ++j)
 #pragma unroll
                 for (int c = j; c < N; ++c)
-                    if (nz(k, j) && nz(k, c)) Hm[j][c] += g[j] * gx(k, c);
+                    if (nz(k, j) && nz(k, c)) Hm[j][c] += g[j] * gr(k, c);
         }
         SocNT W[SSA];
 #pragma unroll
@@ -2058,7 +2178,7 @@ DCOL_HD void launder(P& p) {
 // resume launch, for continuation entry ci (pi = its pair)
 // GLDS: G rows in LDS (Solver; the one-wave-per-workgroup solve kernels only)
 template <int N, int NSOC, int OMAX, int LPP, bool FULL = false, bool BALL = false, bool CONE = false, int OE = 0,
-          int MODE = 0, bool GLDS = false>
+          int MODE = 0, bool GLDS = false, bool BOX = false>
 DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1, int k1o = -1, int k2o = -1) {
     DCOL_STAMP(A, pi, q, 0);
     const int64_t B = A.B;
@@ -2080,7 +2200,8 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1, int k
     make_frame(S2, th2, F2, plain2);
     DCOL_STAMP(A, pi, q, 1);
 
-    using Slv = Solver<N, NSOC, OMAX, LPP, BALL, CONE, OE, GLDS>;
+    static_assert(!BOX || FULL, "BOX kernels are padding-free");
+    using Slv = Solver<N, NSOC, OMAX, LPP, BALL, CONE, OE, GLDS, BOX>;
     Slv P;
     P.q = q;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -2238,7 +2359,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1, int k
 constexpr int kSolveBlock = DCOL_BLOCK;
 static_assert(kSolveBlock % 64 == 0, "one or more whole waves per workgroup");
 
-// FL: variant flags, bit 0 FULL, bit 1 BALL, bit 2 CONE (variants.py)
+// FL: variant flags, bit 0 FULL, bit 1 BALL, bit 2 CONE, bit 3 BOX (variants.py)
 // OE > 0: the row-partitioned (PART) copy with OE extra-column row slots (Solver).
 // FL bit 4 (16): the main launch of a suspend / resume pair (solve_one MODE 1)
 // WPS >= 10: the LDS-rows copy (Solver GLDS) at WPS - 10 waves per SIMD (variants.py);
@@ -2256,7 +2377,7 @@ __global__ void __launch_bounds__(kSolveBlock, WPS % 10) prox_kernel(KArgs A) {
     if (slot >= A.n) return;
     const int64_t pi = A.perm ? (int64_t)A.perm[A.slot0 + slot] : (A.slot0 + slot);
     solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0, OE, (FL & 16) ? 1 : 0,
-              kGlds && WPS >= 10>(A, pi, q);
+              kGlds && WPS >= 10, (FL & 8) != 0>(A, pi, q);
 }
 
 // The resume launch of a suspend / resume pair: one lane group per continuation entry;
@@ -2268,7 +2389,7 @@ __global__ void __launch_bounds__(kSolveBlock, WPS % 10) prox_resume_kernel(KArg
     const int q = (int)(t % LPP);
     if (ci >= A.susp_cap || ci >= (int64_t)*A.susp_count) return;
     const int64_t pi = A.susp_pi[ci];
-    solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0, OE, 2>(A, pi, q, ci);
+    solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0, OE, 2, false, (FL & 8) != 0>(A, pi, q, ci);
 }
 
 }  // namespace dcol

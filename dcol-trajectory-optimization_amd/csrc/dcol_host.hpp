@@ -116,6 +116,12 @@ inline int digest_shape(const dcol_shape_desc& d, int32_t idx, DevShape& S, std:
             S.n_ort = d.nh;
             S.n_p = d.nh;
             S.soc_kind = SOC_NONE;
+            if (d.nh == 6) {   // axis pairs: rows 3..5 the exact negatives of rows 0..2 (BOX kernels)
+                bool bp = true;
+                for (int j = 0; j < 3; ++j)
+                    for (int c = 0; c < 3; ++c) bp = bp && d.A[3 * (j + 3) + c] == -d.A[3 * j + c];
+                S.boxp = bp ? 1 : 0;
+            }
             break;
         case DCOL_SPHERE:     // SOC only   (:151-178)
             S.n_ort = 0;

@@ -11,7 +11,7 @@ namespace dcol {
 // doubles per continuation entry (Solver::SUSP_FIELDS)
 bool susp_available(int N, int nsoc, int omax, int lpp, int flags, int oe, int* fields) {
 #define DCOL_SAV(NN, NS, OM, LP, WP, FL, OEE)                                                      \
-    if (NN == N && NS == nsoc && OM == omax && LP == lpp && OEE == oe && ((FL & 7) & flags) == (FL & 7)) { \
+    if (NN == N && NS == nsoc && OM == omax && LP == lpp && OEE == oe && ((FL & 15) & flags) == (FL & 15)) { \
         if (fields) *fields = Solver<NN, NS, OM, LP, (FL & 2) != 0, (FL & 4) != 0, OEE>::SUSP_FIELDS; \
         return true;                                                                               \
     }
@@ -23,7 +23,7 @@ bool susp_available(int N, int nsoc, int omax, int lpp, int flags, int oe, int* 
 
 hipError_t launch_susp(int N, int nsoc, int omax, int lpp, int flags, int oe, const KArgs& args, hipStream_t stream) {
 #define DCOL_SL(NN, NS, OM, LP, WP, FL, OEE)                                                           \
-    if (NN == N && NS == nsoc && OM == omax && LP == lpp && OEE == oe && ((FL & 7) & flags) == (FL & 7)) { \
+    if (NN == N && NS == nsoc && OM == omax && LP == lpp && OEE == oe && ((FL & 15) & flags) == (FL & 15)) { \
         const int64_t grid = (args.n * LP + kBlock - 1) / kBlock;                                      \
         hipLaunchKernelGGL((prox_kernel<NN, NS, OM, LP, WP, FL, OEE>), dim3(grid), dim3(kBlock), 0, stream, args); \
         hipError_t e = hipGetLastError();                                                              \

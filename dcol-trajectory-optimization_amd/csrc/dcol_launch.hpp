@@ -5,7 +5,7 @@
 
 namespace dcol {
 // launch flags of a bucket (the variant flags FL of variants.py a launch may use)
-enum : int { LF_FULL = 1, LF_BALL = 2, LF_CONE = 4 };
+enum : int { LF_FULL = 1, LF_BALL = 2, LF_CONE = 4, LF_BOX = 8 };
 constexpr int kBlock = kSolveBlock;   // threads per workgroup of the solve kernel
 constexpr int kSideStreams = 7;   // capacity of the extra streams for concurrent variant launches
                                   // (dcol_capi.cpp side_streams(): 3 by default, DCOL_SIDE_STREAMS)

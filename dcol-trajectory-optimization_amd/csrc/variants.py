@@ -36,9 +36,10 @@ workgroups switch on a per-segment variant id (dcol_kernels_fused.hip) — no st
 one launch latency.  Each shape's latency configuration (largest LPP) is in the switch,
 plus the padding-free copies of the FULL shapes; case-4 shapes (N = 7, 8) are not.
 
-Generates dcol_variants.inc (FL = variant flags: bit 0 FULL, bit 1 BALL, bit 2 CONE):
+Generates dcol_variants.inc (FL = variant flags: bit 0 FULL, bit 1 BALL, bit 2 CONE, bit 3 BOX):
   DCOL_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, 0) for every compiled kernel
   DCOL_FULL_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, 1) for the padding-free copies
+  DCOL_BOX_VARIANTS(X)   X(N, NSOC, OMAX, LPP, WPS, 9) for the box x box axis-pair copies
   DCOL_BALL_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, 2) for the ball-SOC copies
   DCOL_CONE_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, 4) for the structured-cone copies
   DCOL_SHAPES(X)    X(N, NSOC, OMAX) once per shape (used by the test emulator)
@@ -114,6 +115,9 @@ CONFIG = {
 # polytope x cone 11.8 -> 12.1e8 pair-solves/s (profiles/r05_b/cls_*.log, two rounds each).
 CONFIG_FL = {(4, 1, 7, 4): [(1, 12)]}
 FULL = {(4, 0)}   # shapes with padding-free copies (see module docstring)
+# BOX copies (FL 9 = FULL | BOX, dcol_device.hpp Solver BOX): box x box pairs in the 12-row
+# bucket, whole axis pairs per lane -- LPP 1 or 2 (an LPP-4 lane holds 3 rows)
+BOX = [(4, 0, 12, 2, 2)]
 # padding-free copies of the structured-cone kernels: (N, NSOC, OMAX) whose pairs commonly
 # fill the bucket (cone x box: the cone's base row + 6 faces = 7)
 FULL_CONE = {(4, 1, 7)}
@@ -209,7 +213,7 @@ def part_variants():
 
 
 # (N, NSOC, OMAX, LPP, WPS, FL without the SUSP bit, OE): the benchmark's poly x poly kernel
-SUSP = [(4, 0, 12, 2, 2, 1, 0)]
+SUSP = [(4, 0, 12, 2, 2, 9, 0), (4, 0, 12, 2, 2, 1, 0)]   # the BOX copy first (box x box launches)
 
 FUSE_PART_OMAX = 6   # PART buckets in the fused kernel: the small ones (its compile time grows with its cases)
 
@@ -255,6 +259,8 @@ def main():
     lines += [f"    X({n}, {s}, {o}, {l}, {w}, 0) \\" for n, s, o in shapes for l, w in configs(n, s, o)]
     lines += ["", "#define DCOL_FULL_VARIANTS(X) \\"]
     lines += [f"    X({n}, {s}, {o}, {l}, {w}, 1) \\" for n, s, o in shapes if (n, s) in FULL for l, w in configs(n, s, o)]
+    lines += ["", "#define DCOL_BOX_VARIANTS(X) \\"]
+    lines += [f"    X({n}, {s}, {o}, {l}, {w}, 9) \\" for n, s, o, l, w in BOX]
     lines += ["", "#define DCOL_FULL_CONE_VARIANTS(X) \\"]
     lines += [f"    X({n}, {s}, {o}, {l}, {w}, 5) \\" for n, s, o in shapes if (n, s, o) in FULL_CONE
               for l, w in configs_fl(n, s, o, 4)]

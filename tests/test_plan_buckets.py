@@ -19,8 +19,9 @@ def _solves(plan):
 
 def test_benchmark_batch_is_one_padding_free_two_lane_bucket(engine):
     """configs[3] (100k random rectangular-prism pairs, bench.py): one bucket, the padding-free
-    (4, 0, 12) polytope x polytope kernel at two lanes per pair -- the kernel the roofline line
-    and the rocprofv3 summaries in profiles/ describe."""
+    (4, 0, 12) box x box (axis-pair, flags 1 | 8) kernel at two lanes per pair -- the kernel the
+    roofline line and the rocprofv3 summaries in profiles/ describe; with DCOL_NO_BOX the
+    padding-free dense-row one (flags 1, test_box_disabled_by_env)."""
     import bench
     tab = bench.shape_table(64, 0)
     s1, s2 = bench.pairs(100_000, 64, 0)[:2]
@@ -28,8 +29,24 @@ def test_benchmark_batch_is_one_padding_free_two_lane_bucket(engine):
     plan = engine.plan(ids[s1], ids[s2], cache=False)
     b = plan.buckets()
     assert len(b) == 1 and plan.num_launches == 1
-    assert b[0] == {"kind": "solve", "N": 4, "nsoc": 0, "omax": 12, "lpp": 2, "oe": 0, "flags": 1, "status": 0,
+    assert b[0] == {"kind": "solve", "N": 4, "nsoc": 0, "omax": 12, "lpp": 2, "oe": 0, "flags": 9, "status": 0,
                     "pairs": 100_000}
+
+
+def test_box_needs_exact_axis_pairs(engine):
+    """The BOX bucket takes only pairs of 6-row polytopes whose rows 3..5 are the exact
+    negatives of rows 0..2: a prism with one face normal perturbed, or rows in another order,
+    stays in the dense-row 12-row bucket (flags 1)."""
+    import bench
+    tab = bench.shape_table(4, 0)
+    tab["A_pool"] = tab["A_pool"].copy()
+    tab["A_pool"][6 + 4] = [0.0, -1.0, 1e-12]           # shape 1: face 4 no longer -face 1
+    tab["A_pool"][12:18] = tab["A_pool"][12:18][[0, 3, 1, 4, 2, 5]]   # shape 2: pairs interleaved
+    ids = _ids(engine, tab)
+    s1 = np.array([0, 0, 1, 2, 3], np.int32)
+    s2 = np.array([3, 1, 0, 3, 0], np.int32)
+    b = {(x["flags"], x["pairs"]) for x in engine.plan(ids[s1], ids[s2], cache=False).buckets() if x["kind"] == "solve"}
+    assert b == {(9, 2), (1, 3)}, b
 
 
 def _polygon_box(engine, B, seed=0):
