@@ -8,8 +8,9 @@ pair); poses r ~ U(-3, 3)^3, p (MRP) ~ U(-1, 1)^3; seed 0 (+ rank).  One "step" 
 dcol_plan_run over the whole batch: conic assembly + PDIP (pdip_tol 1e-6) + the 12-gradient
 (FD mode = the reference's formulation) + alpha, with poses already resident in HBM.
 `value` / `ms_per_step` are the one-stream run: K steps issued back to back on one HIP
-stream, each bracketed by HIP events on that stream, so `kernel_ms` (the mean of those
-event intervals) and the rooflines come from the same run and ms_per_step >= kernel_ms.
+stream; `kernel_ms` is the HIP-event time of that same timed region on the launch stream / K
+(the per-launch duration of back-to-back launches), so the rooflines come from the same run
+and ms_per_step >= kernel_ms.
 Beside it, `pipeline`: the same steps issued round-robin on --streams (default 2) streams
 with their own output buffers, as a pipelined batch service would (the last, partly-filled
 round of one step's waves overlaps the first round of the next) -- an overlap rate, never
@@ -289,22 +290,31 @@ def main():
         step()
     sync(dev, wd, "warmup")
 
-    # value: exactly K steps on ONE stream, barrier + synchronize on both sides; each step
-    # bracketed by HIP events on that stream (the kernel duration of this same run)
+    # value: exactly K steps on ONE stream, barrier + synchronize on both sides.  kernel_ms =
+    # the HIP-event time of that same timed region on the launch stream / K: the per-launch
+    # duration of the back-to-back launches (one event pair: a pair around every launch costs
+    # ~7.5 us of GPU time per step, tools/step_gap.py).  With a deadline (N > 1) every 4th step
+    # is followed by an untimed event, so a rank that hangs names the step.
     barrier(dist, wd, "barrier before the timed steps")
     sync(dev, wd, "synchronize before the timed steps")
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    e_start, e_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    marks = []
     t0 = time.perf_counter()
+    e_start.record(stream)
     for k in range(args.steps):
-        ev[k][0].record(stream)
         step()
-        ev[k][1].record(stream)
-    for k in range(args.steps):       # (a rank that hangs names its step)
-        wait_event(ev[k][1], wd, "solve", k)
+        if wd is not None and (k % 4 == 3 or k == args.steps - 1):
+            e = torch.cuda.Event()
+            e.record(stream)
+            marks.append((k, e))
+    e_end.record(stream)
+    for k, e in marks:
+        wait_event(e, wd, "solve", k)
+    wait_event(e_end, wd, "solve", args.steps - 1)
     sync(dev, wd, "synchronize after the timed steps")
     elapsed = time.perf_counter() - t0
     barrier(dist, wd, "barrier after the timed steps")
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_ms = e_start.elapsed_time(e_end) / args.steps
 
     # pipeline: the same K steps round-robin on S streams (an overlap rate, reported beside)
     elapsed_pipe = None
@@ -386,8 +396,9 @@ def main():
                           "flops_per_pair": flops_pair,
                           "flops_source": "op-counting C restatement, profiles/flop_model.json"
                           if os.path.exists(os.path.join(REPO, "profiles", "flop_model.json")) else "hand model"},
-        "timing": "value = pairs / ms_per_step of K steps on one stream; kernel_ms = the mean HIP-event duration "
-                  "of those same K launches (events on the launch stream), the rooflines' time base",
+        "timing": "value = pairs / ms_per_step of K steps on one stream; kernel_ms = the HIP-event time of that same "
+                  "timed region on the launch stream / K (the per-launch duration of the back-to-back launches), the "
+                  "rooflines' time base",
         "pipeline": {"streams": S, "note": "the same K steps issued round-robin on S streams with separate outputs "
                      "(an overlap rate: one step's last round of waves overlaps the next step's first; not value)",
                      "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),

@@ -1123,6 +1123,9 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
             a.susp_pi = nullptr;
             a.susp_state = nullptr;
             a.susp_cap = 0;
+#ifdef DCOL_STAMPS
+            a.stamps = d->stamps;   // (diagnostic build) solve_one's phase stamps of each request
+#endif
             h->flags = kflags;
             h->tol = tol;
             h->max_iter = max_iter;
@@ -1196,6 +1199,19 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
     if (iters) *iters = h->iters;
     if (status) *status = h->status;
     return DCOL_SUCCESS;
+}
+
+int dcol_debug_pair_stamps(const dcol_table* tc, uint64_t out[16]) {
+    if (!tc || !out) return fail(DCOL_ERR_ARG, "dcol_debug_pair_stamps: NULL argument");
+#ifdef DCOL_STAMPS
+    dcol_table* t = const_cast<dcol_table*>(tc);
+    std::lock_guard<std::mutex> lk(t->mu);
+    if (!t->pair_host) return fail(DCOL_ERR_ARG, "dcol_debug_pair_stamps: no pair call yet");
+    for (int k = 0; k < 16; ++k) out[k] = __atomic_load_n(&t->pair_host->stamps[k], __ATOMIC_ACQUIRE);
+    return DCOL_SUCCESS;
+#else
+    return fail(DCOL_ERR_ARG, "dcol_debug_pair_stamps: not a stamps build (make stamps)");
+#endif
 }
 
 int dcol_table_stop_pair_server(const dcol_table* tc) {

@@ -183,7 +183,8 @@ struct KArgs {
     double* susp_state;                 // [fields][susp_cap]: it, x[N], then (s, z, r) per lane row
     int64_t susp_cap;
 #ifdef DCOL_STAMPS
-    unsigned long long* stamps;         // diagnostic build only (tools/stamp_probe.hip): [B][16]
+    unsigned long long* stamps = nullptr;   // diagnostic build only (tools/stamp_probe.hip, the pair
+                                            // server of lib_stamps): [B][16]; nullptr: none
 #endif
 };
 
@@ -194,7 +195,7 @@ struct KArgs {
         unsigned long long t_;                                                          \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");      \
         __builtin_amdgcn_sched_barrier(0);                                              \
-        if ((q) == 0) (A).stamps[16 * (pi) + (k)] = t_;                                 \
+        if ((q) == 0 && (A).stamps) (A).stamps[16 * (pi) + (k)] = t_;                   \
     } while (0)
 // sub-phases of PDIP iteration 2 into stamps[16 * pi + 8 + k] (Solver::dbg); with
 // DCOL_STAMPS_INIT the sub-phases of initialize() instead (DCOL_NSTAMP)
@@ -2212,7 +2213,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1, int k
     }
 #endif
 #ifdef DCOL_STAMPS
-    P.dbg = (q == 0) ? A.stamps + 16 * pi + 8 : nullptr;
+    P.dbg = (q == 0 && A.stamps) ? A.stamps + 16 * pi + 8 : nullptr;
 #endif
     P.assemble(A, S1, S2, F1, F2);
     DCOL_STAMP(A, pi, q, 2);

@@ -66,8 +66,8 @@ __global__ void __launch_bounds__(kSolveBlock, 1) prox_pair_server(KArgs Args, P
         const int32_t req = (int32_t)(r >> 32);
         if (req == last) {
             if (!stop && wall_clock64() - t0 < idle_ticks) {
-                __builtin_amdgcn_s_sleep(2);
-                for (int i = 0; i < poll_sleep; ++i) __builtin_amdgcn_s_sleep(127);   // (A/B knob)
+                if (poll_sleep >= 0) __builtin_amdgcn_s_sleep(2);   // (A/B knob: < 0 polls without sleeping)
+                for (int i = 0; i < poll_sleep; ++i) __builtin_amdgcn_s_sleep(127);
                 continue;
             }
             // leaving: clear alive, then look at the request word once more -- a caller that
@@ -118,6 +118,10 @@ __global__ void __launch_bounds__(kSolveBlock, 1) prox_pair_server(KArgs Args, P
         if (threadIdx.x == 0) {   // request-to-answer time on the device (dcol_table_pair_stats)
             box->solve_ticks = wall_clock64() - w0;
             box->solve_cycles = clock64() - c0;
+#ifdef DCOL_STAMPS
+            box->stamps[6] = (unsigned long long)c0;
+            box->stamps[7] = (unsigned long long)clock64();
+#endif
         }
         // the pair's lanes reconverged: the fence waits for all of the wave's output stores
         __threadfence_system();

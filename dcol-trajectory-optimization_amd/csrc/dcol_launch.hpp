@@ -58,6 +58,12 @@ struct PairBox {
     int32_t done, alive, stop;
     int32_t xcd;   // the XCD the running server sits on (HW_REG_XCC_ID; dcol_table_pair_stats)
     int64_t solve_ticks, solve_cycles;   // the last served request: wall-clock ticks and shader cycles
+#ifdef DCOL_STAMPS
+    // diagnostic build (make stamps): s_memtime at solve_one's phases (DCOL_STAMP 0..5: start,
+    // frames, assembly, initialise, PDIP loop, gradient; 8..15: the sub-phases of PDIP
+    // iteration 2), the request seen (6) and the answer's release (7); dcol_debug_pair_stamps
+    unsigned long long stamps[16];
+#endif
 };
 constexpr int kPairBoxIdBits = 24;
 // a server on `stream` serving box (device view) with args' table pointers, flags, tolerance

@@ -193,6 +193,9 @@ PART = {
 PART_FL = {
     (6, 2, 4, 4, "ball"): [(2, 2)],
     (6, 2, 6, 6, "ball"): [(2, 2), (1, 1)],
+    # (cone x polygon / polygon x cone with LDS rows at two waves per SIMD -- WPS 12, 19 scratch
+    # instructions per loop against 100 with register rows, tools/isa_stats.py 6:2:8:2:6:32
+    # --waves 2 -- measured 1-2 % slower: 6.08 -> 5.97-6.02e8, profiles/r05_lds/i_cls_*.log)
 }
 
 

@@ -65,6 +65,7 @@ SIGNATURES = {
     "dcol_table_pair_plans": (c_int, [c_void_p, POINTER(c_int32)]),
     "dcol_table_pair_stats": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64),
                                       POINTER(c_double), POINTER(c_double), POINTER(c_int32)]),
+    "dcol_debug_pair_stamps": (c_int, [c_void_p, c_void_p]),
     "dcol_table_stop_pair_server": (c_int, [c_void_p]),
     "dcol_table_pair_server_running": (c_int, [c_void_p, POINTER(c_int32)]),
     "dcol_shutdown": (c_int, []),

@@ -218,6 +218,11 @@ int dcol_table_pair_stats(const dcol_table* table, int64_t* served, int64_t* lau
                           int64_t* server_starts, double* server_solve_us, double* server_solve_cycles,
                           int32_t* server_xcd);
 
+/* Diagnostic (the stamps build, `make stamps` -> lib_stamps/): the shader-clock stamps of the
+ * last request the pair server answered -- [0..5] solve start, frames, assembly, initialise,
+ * PDIP loop end, gradient end; [6] request seen, [7] answer released; [8..15] sub-phases of
+ * PDIP iteration 2.  DCOL_ERR_ARG in the product build.                                    */
+int dcol_debug_pair_stamps(const dcol_table* table, uint64_t out[16]);
 /* Stop this table's pair server now, if one is resident (waiting at most 5 s for it to
  * leave); the next dcol_prox_pair starts a new one.  E.g. before a long batch phase, so no
  * wave polls the mailbox meanwhile.                                                      */
