@@ -113,7 +113,12 @@ CONFIG = {
 # kernel: 349 VGPRs at one wave -> 256 at two waves with 18 scratch instructions per loop
 # (tools/isa_stats.py 4:1:7:1:0:37 --waves 2), bitwise equal; cone x polytope 11.8 -> 12.2e8,
 # polytope x cone 11.8 -> 12.1e8 pair-solves/s (profiles/r05_b/cls_*.log, two rounds each).
-CONFIG_FL = {(4, 1, 7, 4): [(1, 12)]}
+CONFIG_FL = {(4, 1, 7, 4): [(1, 12)],
+             # sphere x box: LDS rows at one lane per pair, two waves per SIMD -- 19.1 loop
+             # instructions per pair-iteration against 30.5 for the LPP-2 kernel, whose second
+             # lane idles through the SOC block (tools/isa_stats.py 4:1:6:1:0:34 --waves 2: 29
+             # scratch instructions per loop); the LPP-2 copy stays for small plans
+             (4, 1, 6, 2): [(1, 12), (2, 2)]}
 FULL = {(4, 0)}   # shapes with padding-free copies (see module docstring)
 # BOX copies (FL 9 = FULL | BOX, dcol_device.hpp Solver BOX): box x box pairs in the 12-row
 # bucket, whole axis pairs per lane -- LPP 1 or 2 (an LPP-4 lane holds 3 rows)
