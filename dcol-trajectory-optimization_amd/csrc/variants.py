@@ -122,7 +122,10 @@ CONFIG_FL = {(4, 1, 7, 4): [(1, 12)],
 FULL = {(4, 0)}   # shapes with padding-free copies (see module docstring)
 # BOX copies (FL 9 = FULL | BOX, dcol_device.hpp Solver BOX): box x box pairs in the 12-row
 # bucket, whole axis pairs per lane -- LPP 1 or 2 (an LPP-4 lane holds 3 rows)
-BOX = [(4, 0, 12, 2, 2)]
+# three waves per SIMD: 168 VGPRs, the PDIP loop spill-free (72 B of scratch outside it);
+# against two waves (profiles/r05_box3/, interleaved): 100k serial 2.06-2.18e9 = unchanged,
+# pipelined 2.59-2.76 -> 3.10-3.15e9, 1M kernel-only 2.87-2.97 -> 2.96-3.05e9
+BOX = [(4, 0, 12, 2, 3)]
 # padding-free copies of the structured-cone kernels: (N, NSOC, OMAX) whose pairs commonly
 # fill the bucket (cone x box: the cone's base row + 6 faces = 7)
 FULL_CONE = {(4, 1, 7)}
