@@ -125,6 +125,9 @@ FULL = {(4, 0)}   # shapes with padding-free copies (see module docstring)
 # three waves per SIMD: 168 VGPRs, the PDIP loop spill-free (72 B of scratch outside it);
 # against two waves (profiles/r05_box3/, interleaved): 100k serial 2.06-2.18e9 = unchanged,
 # pipelined 2.59-2.76 -> 3.10-3.15e9, 1M kernel-only 2.87-2.97 -> 2.96-3.05e9
+# measured slower, not built (profiles/r05_o/, r05_q/): four waves with LDS rows (4, 0, 12, 2, 14)
+# -- 24 scratch accesses per loop, 87 us per 100k; one lane per pair with LDS rows at two
+# waves (4, 0, 12, 1, 12) -- spill-free, 64.5 us per 100k, 2.54e9 at 1M
 BOX = [(4, 0, 12, 2, 3)]
 # padding-free copies of the structured-cone kernels: (N, NSOC, OMAX) whose pairs commonly
 # fill the bucket (cone x box: the cone's base row + 6 faces = 7)
