@@ -80,6 +80,21 @@ int side_streams() {
     }();
     return n;
 }
+// side streams a plan that fills the GPU fans out over: 2 -- three buckets in flight with the
+// caller's stream.  Fewer concurrent buckets finish a large mixed step sooner: the
+// one-wave-per-SIMD kernels (400-500 registers) need a whole SIMD's register file and wait
+// behind co-running buckets' waves when four run at once (1M mixed plan, synchronised
+// steps: 0.87 ms at 2 against 0.94 ms at 3 and 1).  A small plan (its
+// buckets cannot fill the GPU, each runs its latency configuration) keeps every side
+// stream.  DCOL_SIDE_STREAMS_LARGE=<1..side_streams()> for A/B runs.
+int large_side_streams() {
+    static const int n = [] {
+        const char* e = std::getenv("DCOL_SIDE_STREAMS_LARGE");
+        const int v = e ? std::atoi(e) : 2;
+        return v < 1 ? 1 : (v > side_streams() ? side_streams() : v);
+    }();
+    return n;
+}
 
 // dcol_prox_pair's one-pair server: how long (us) it stays resident without a request
 // (DCOL_PAIR_SERVER_IDLE_US, default 1000); DCOL_PAIR_SERVER=0: no server, one launch per
@@ -213,6 +228,7 @@ struct dcol_plan {
     bool owns = false;           // device arrays owned (false: views into table staging)
     std::vector<Launch> launches;
     int lanes = 1;               // streams the launches are spread over (1 = serial)
+    bool small = false;          // the plan cannot fill the GPU (bucket_pairs: small_plan)
     std::vector<int> issue;      // launch issue order (assign_lanes: longest first); empty = as built
     hipEvent_t fork = nullptr;   // recorded on the caller's stream, awaited by the side streams
     hipEvent_t join[kSideStreams] = {};
@@ -575,6 +591,7 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
         p->launches.push_back(L);
     }
     for (int64_t i = 0; i < B; ++i) perm[(size_t)groups[gid[i]].at++] = (int32_t)i;   // stable
+    p->small = small_plan;
     assign_lanes(p);
     return DCOL_SUCCESS;
 }
@@ -600,7 +617,7 @@ void assign_lanes(dcol_plan* p) {
     p->lanes = 1;
     p->issue.clear();
     if (solves < 2) return;
-    const int lanes = std::min(solves, side_streams() + 1);
+    const int lanes = std::min(solves, (p->small ? side_streams() : large_side_streams()) + 1);
     std::vector<int> order;
     std::vector<double> cost(p->launches.size(), 0.0);
     for (size_t i = 0; i < p->launches.size(); ++i) {

@@ -20,6 +20,9 @@ def cost(b):
     return b["pairs"] * per * (0.5 if b["nsoc"] == 0 else 1.0)
 
 
+if "--steps" in sys.argv:   # torch's HIP context first (as bench.py does), then the engine's
+    import torch
+    torch.zeros(1, device="cuda:0")
 tab = bench.mixed_table()
 s1, s2, _, _ = bench.mixed_pairs(tab, 1_000_000, seed=0)
 eng = Engine(device=0)
