@@ -183,6 +183,9 @@ PART = {
     # (LDS rows at one wave per SIMD -- WPS 11, fewer values parked in AGPRs -- measured slower
     # here: capsule x polytope -5 %, cylinder x polytope -10 %, polygon x polytope +-0
     # (profiles/r05_b/cls_*.log); the register rows stay)
+    # (two lanes per pair at two waves per SIMD -- (8, 2): 5 scratch accesses per loop, (10, 2): 19
+    # -- measured slower too: capsule x polytope -1 %, cylinder x polytope -7 % alone, the 1M
+    # mixed step 0.874-0.876 -> 0.879-0.887 ms; profiles/r05_y/, r05_z/)
     (5, 1): {(8, 2): [(1, 1), (2, 1)], (10, 2): [(1, 1), (2, 1)], (14, 2): [(2, 1)], (18, 2): [(2, 1)]},
     # x sphere / cone: both lanes own a SOC block (capsule x sphere 11.2e8 at LPP 2, 9.1e8 at 1)
     # two waves per SIMD where the allocator then spills at most a few scratch accesses per
