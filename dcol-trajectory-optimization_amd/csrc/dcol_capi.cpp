@@ -867,6 +867,12 @@ int dcol_plan_num_launches(const dcol_plan* p, int32_t* n) {
     return DCOL_SUCCESS;
 }
 
+int dcol_plan_num_streams(const dcol_plan* p, int32_t* n) {
+    if (!p || !n) return fail(DCOL_ERR_ARG, "dcol_plan_num_streams: NULL argument");
+    *n = p->fused() ? 1 : p->lanes;
+    return DCOL_SUCCESS;
+}
+
 int dcol_plan_num_buckets(const dcol_plan* p, int32_t* n) {
     if (!p || !n) return fail(DCOL_ERR_ARG, "dcol_plan_num_buckets: NULL argument");
     *n = (int32_t)p->launches.size();

@@ -130,6 +130,8 @@ class Plan:
         self.num_launches = int(n.value)       # kernel launches per run
         _lib.check(lib.dcol_plan_num_buckets(h, ctypes.byref(n)), "dcol_plan_num_buckets")
         self.num_buckets = int(n.value)        # variant buckets (incl. rejected pairs)
+        _lib.check(lib.dcol_plan_num_streams(h, ctypes.byref(n)), "dcol_plan_num_streams")
+        self.num_streams = int(n.value)        # streams a run's launches are spread over
 
     def buckets(self) -> list:
         """The plan's variant buckets (dcol_plan_bucket): one dict per bucket with kind

@@ -152,6 +152,8 @@ int dcol_plan_create_ex(const dcol_table* table, int64_t B, const int32_t* shape
                         const int32_t* shape2, int32_t options, dcol_plan** out);
 int dcol_plan_destroy(dcol_plan* plan);
 int dcol_plan_num_launches(const dcol_plan* plan, int32_t* n); /* kernel launches per run */
+int dcol_plan_num_streams(const dcol_plan* plan, int32_t* n); /* streams a run spreads its launches over:
+                                                                  the caller's + side streams (1 = caller's only) */
 int dcol_plan_num_buckets(const dcol_plan* plan, int32_t* n);  /* variant buckets (incl. rejects) */
 /* Bucket i (0 <= i < dcol_plan_num_buckets) of a plan, for tests and tools: info[0] kind (0 a
  * solve bucket, 1 rejected pairs), [1] N (primal columns), [2] SOC blocks, [3] orthant-row

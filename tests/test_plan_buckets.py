@@ -92,3 +92,27 @@ def test_bucket_index_checked(engine):
     n = ctypes.c_int64()
     with pytest.raises(DcolLibraryError):
         _lib.check(_lib.load().dcol_plan_bucket(plan.handle, plan.num_buckets, info, ctypes.byref(n)), "dcol_plan_bucket")
+
+
+def test_fanout_width_by_plan_size(engine):
+    """A mixed plan that fills the GPU spreads its buckets over the caller's stream + 2 side
+    streams (three buckets in flight: DESIGN.md section 5, "Two side streams"); a small one,
+    whose buckets run their latency configurations, over the caller's + 3; a fused small plan
+    and a one-bucket plan run on the caller's stream alone."""
+    import os
+    import bench
+    if os.environ.get("DCOL_SIDE_STREAMS") or os.environ.get("DCOL_SIDE_STREAMS_LARGE") or os.environ.get("DCOL_NO_FANOUT"):
+        pytest.skip("fan-out width overridden by the environment")
+    tab = bench.mixed_table()
+    ids = _ids(engine, tab)
+    s1, s2 = bench.mixed_pairs(tab, 150_000, seed=3)[:2]
+    big = engine.plan(ids[s1], ids[s2], cache=False)
+    assert len(_solves(big)) > 4 and big.num_streams == 3
+    small = engine.plan(ids[s1[:2000]], ids[s2[:2000]], cache=False, fuse=False)
+    assert len(_solves(small)) > 4 and small.num_streams == 4
+    fused = engine.plan(ids[s1[:2000]], ids[s2[:2000]], cache=False)
+    assert fused.num_streams == (1 if fused.num_launches == 1 else 4)
+    tb = bench.shape_table(64, 0)
+    idb = _ids(engine, tb)
+    b1, b2 = bench.pairs(100_000, 64, 0)[:2]
+    assert engine.plan(idb[b1], idb[b2], cache=False).num_streams == 1
