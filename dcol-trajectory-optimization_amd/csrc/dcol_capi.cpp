@@ -295,7 +295,10 @@ hipError_t launch_variant(int N, int nsoc, int omax, int lpp, int flags, const K
         if (N == 5 && nsoc == 1) return launch_part_n5s1(omax, oe, lpp, flags, a, st);
         if (N == 5 && nsoc == 2) return launch_part_n5s2(omax, oe, lpp, flags, a, st);
         if (N == 6 && nsoc == 1) return launch_part_n6s1(omax, oe, lpp, flags, a, st);
-        if (N == 6 && nsoc == 2) return launch_part_n6s2(omax, oe, lpp, flags, a, st);
+        if (N == 6 && nsoc == 2) {   // the ball-row copies first (a bucket's list order), then the dense ones
+            const hipError_t e = launch_part_n6s2(omax, oe, lpp, flags, a, st);
+            return e == hipErrorInvalidValue ? launch_part_n6s2_dense(omax, oe, lpp, flags, a, st) : e;
+        }
         return hipErrorInvalidValue;
     }
     if (N == 4) return launch_n4(nsoc, omax, lpp, flags, a, st);

@@ -19,6 +19,7 @@ hipError_t launch_part_n5s1(int omax, int oe, int lpp, int flags, const KArgs& a
 hipError_t launch_part_n5s2(int omax, int oe, int lpp, int flags, const KArgs& args, hipStream_t stream);
 hipError_t launch_part_n6s1(int omax, int oe, int lpp, int flags, const KArgs& args, hipStream_t stream);
 hipError_t launch_part_n6s2(int omax, int oe, int lpp, int flags, const KArgs& args, hipStream_t stream);
+hipError_t launch_part_n6s2_dense(int omax, int oe, int lpp, int flags, const KArgs& args, hipStream_t stream);
 
 // One bucket of a fused launch (dcol_kernels_fused.hip): workgroups [block0, next block0)
 // solve plan slots [slot0, slot0 + n) with fused variant `vid` (DCOL_FUSED_VARIANTS),
@@ -83,7 +84,7 @@ hipError_t launch_pair_server(const KArgs& args, PairBox* box, int64_t idle_tick
         if (reset) (void)hipMemcpyToSymbol(HIP_SYMBOL(dcol_exec_violations), &z, sizeof(z));   \
         return v;                                                                              \
     }
-#define DCOL_EXEC_TAGS(X) X(n4) X(n5) X(n6) X(n7) X(n8) X(fused) X(p51) X(p52) X(p61) X(p62) X(susp) X(server)
+#define DCOL_EXEC_TAGS(X) X(n4) X(n5) X(n6) X(n7) X(n8) X(fused) X(p51) X(p52) X(p61) X(p62) X(p62d) X(susp) X(server)
 #define DCOL_EXEC_DECL(tag) unsigned long long exec_violations_##tag(bool reset);
 DCOL_EXEC_TAGS(DCOL_EXEC_DECL)
 DCOL_EXEC_DECL(capi)   // the C-ABI unit's own counter (dcol_debug_exec_selftest)
