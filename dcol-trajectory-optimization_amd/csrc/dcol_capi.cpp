@@ -268,12 +268,16 @@ bool stop_pair_server(dcol_table* t, int timeout_ms) {
     return true;
 }
 
-// A batch launch on `device` asks every resident pair server there to leave (it does after
+// A batch launch that can fill `device` (a plan that is not small: bucket_pairs) asks every
+// resident pair server there to leave (it does after
 // the request in hand, at its next poll), without waiting: a kernel resident beside a batch
 // plan slowed the plan by 1.3-2x depending on the server stream's kind and the number of
 // hardware queues (tools/server_tax.py, profiles/r05_d/, r05_e/), so the latency path gives
 // way to the throughput path.  The table's next dcol_prox_pair drains it and starts a new
-// server (one launch, ~10 us).
+// server (one launch, ~10 us).  Small plans (ALTRO-sized batches, one-pair launches) leave it
+// resident: a caller interleaving them with drop-in calls would otherwise restart the server
+// at nearly every pair call, and a latency-bound plan of a few waves is not what the
+// server's hardware-queue tax was measured on.
 void yield_pair_servers(int device) {
     if (g_server_tables.load(std::memory_order_acquire) == 0) return;
     static const bool off = [] {   // DCOL_PAIR_SERVER_YIELD=0: the server stays (A/B: tools/server_tax.py)
@@ -283,9 +287,11 @@ void yield_pair_servers(int device) {
     if (off) return;
     std::lock_guard<std::mutex> lk(g_tables_mu);
     for (dcol_table* t : g_tables) {
-        if (t->device != device || !t->pair_host) continue;
-        if (!__atomic_load_n(&t->pair_host->alive, __ATOMIC_ACQUIRE)) continue;
-        __atomic_store_n(&t->pair_host->stop, 1, __ATOMIC_SEQ_CST);
+        // (pair_host is published by dcol_prox_pair with a release store after its memset)
+        PairBox* h = __atomic_load_n(&t->pair_host, __ATOMIC_ACQUIRE);
+        if (t->device != device || !h) continue;
+        if (!__atomic_load_n(&h->alive, __ATOMIC_ACQUIRE)) continue;
+        __atomic_store_n(&h->stop, 1, __ATOMIC_SEQ_CST);
         t->stop_req.store(true, std::memory_order_release);
     }
 }
@@ -383,16 +389,21 @@ int dcol_table_create(const dcol_shape_desc* shapes, int32_t n, int32_t device, 
 
 int dcol_table_destroy(dcol_table* t) {
     if (!t) return DCOL_SUCCESS;
+    DeviceGuard g(t->device);
+    // the server exits at its next poll; one that does not (a hung device) keeps the whole
+    // table -- its wave may still read the shape table and the mailbox -- registered, so that
+    // dcol_shutdown still sees it and can stop it before the process's HIP context goes away,
+    // and the call fails.  Only a table whose server has left is unregistered and freed.
+    {
+        std::lock_guard<std::mutex> tl(t->mu);
+        if (!stop_pair_server(t, kServerStopMs))
+            return fail(DCOL_ERR_HIP, "dcol_table_destroy: the pair server did not stop within 5 s (table kept)");
+    }
     {
         std::lock_guard<std::mutex> lk(g_tables_mu);
         g_tables.erase(std::remove(g_tables.begin(), g_tables.end(), t), g_tables.end());
         if (t->server_launched) g_server_tables.fetch_sub(1, std::memory_order_acq_rel);
     }
-    DeviceGuard g(t->device);
-    // the server exits at its next poll; one that does not (a hung device) keeps the whole
-    // table -- its wave may still read the shape table and the mailbox -- and the call fails
-    if (!stop_pair_server(t, kServerStopMs))
-        return fail(DCOL_ERR_HIP, "dcol_table_destroy: the pair server did not stop within 5 s (table leaked)");
     for (auto& kv : t->pair_lru) dcol_plan_destroy(kv.second);
     if (t->pair_stream) (void)hipStreamDestroy(t->pair_stream);
     if (t->server_stream) (void)hipStreamDestroy(t->server_stream);
@@ -903,7 +914,7 @@ int plan_run_rec(const dcol_plan* p, const double* pose1, const double* pose2, d
                  int32_t flags, double* alpha, double* contact, double* grad, int32_t* iters, int32_t* status,
                  double* rec, void* stream, bool yield = true) {
     if (!p) return fail(DCOL_ERR_ARG, "dcol_plan_run: NULL plan");
-    if (yield) yield_pair_servers(p->table->device);   // (the pair call's own launch path keeps it)
+    if (yield && !p->small) yield_pair_servers(p->table->device);   // (the pair call's own launch path keeps it)
     if (p->B == 0) return DCOL_SUCCESS;
     if (!pose1 || !pose2 || (!alpha && !rec))
         return fail(DCOL_ERR_ARG, "dcol_plan_run: pose1, pose2 and alpha are required");
@@ -1011,13 +1022,14 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
         // fine-grained coherent on purpose: the server's handshake (system-scope atomics on
         // req / done / alive / stop) needs host and device to see each other's stores while
         // the wave runs, whatever HIP_HOST_COHERENT says
-        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&t->pair_host), sizeof(PairBox),
+        PairBox* hb = nullptr;
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&hb), sizeof(PairBox),
                                      hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent);
         if (e == hipSuccess) {
-            std::memset(t->pair_host, 0, sizeof(PairBox));   // flags and sequence numbers start at 0
-            t->pair_host->xcd = -1;                           // no server yet
+            std::memset(hb, 0, sizeof(PairBox));   // flags and sequence numbers start at 0
+            hb->xcd = -1;                           // no server yet
         }
-        if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&t->pair_dev), t->pair_host, 0);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&t->pair_dev), hb, 0);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&t->pair_stream, hipStreamNonBlocking);
         // The server stream: a CU-masked stream (mask = every CU), because HIP never pools a
         // CU-masked stream into a shared hardware queue -- the resident server gets a queue of
@@ -1051,14 +1063,16 @@ int dcol_prox_pair(const dcol_table* tc, int32_t s1, int32_t s2, const double* p
             (void)hipGetLastError();
             khz = 0;
         }
-        if (e != hipSuccess) {
-            if (t->pair_host) (void)hipHostFree(t->pair_host);
+        if (e != hipSuccess) {   // (never published: nothing else has seen hb)
+            if (hb) (void)hipHostFree(hb);
             if (t->pair_stream) (void)hipStreamDestroy(t->pair_stream);
-            t->pair_host = t->pair_dev = nullptr;
+            t->pair_dev = nullptr;
             t->pair_stream = nullptr;
             return fail(DCOL_ERR_HIP, std::string("dcol_prox_pair staging: ") + hipGetErrorString(e));
         }
         t->wall_ticks_us = khz > 0 ? (int64_t)khz / 1000 : 0;
+        // published after its initialisation: yield_pair_servers reads it without t->mu
+        __atomic_store_n(&t->pair_host, hb, __ATOMIC_RELEASE);
     }
     const int64_t key = (int64_t)s1 * ns + s2;
     const bool c4 = (flags & DCOL_CASE4) != 0;

@@ -23,7 +23,7 @@ GRAD_ANY = GRAD_FD | GRAD_ENVELOPE | GRAD_IMPLICIT
 # enum dcol_plan_options
 PLAN_CASE4, PLAN_NO_FUSE, PLAN_SUSPEND = 1, 2, 4
 SUCCESS, ERR_ARG, ERR_HIP, ERR_NOMEM = 0, -1, -2, -3
-ABI_VERSION = 3
+ABI_VERSION = 4
 PAIR_PLANS_MAX = 64   # DCOL_PAIR_PLANS_MAX
 
 
@@ -98,12 +98,21 @@ def load(path: str | None = None):
     except OSError as e:  # pragma: no cover - environment specific
         _load_error = f"cannot load {p}: {e}"
         raise DcolLibraryError(_load_error) from e
+    # the version first: a stale library lacks some of the entry points bound below, and
+    # must fail with this message rather than a bare AttributeError from getattr
+    try:
+        ver_fn = lib.dcol_abi_version
+    except AttributeError as e:
+        raise DcolLibraryError(f"{p}: no dcol_abi_version export (not a libdcol build)") from e
+    ver_fn.restype = ctypes.c_int
+    ver_fn.argtypes = []
+    if ver_fn() != ABI_VERSION:
+        raise DcolLibraryError(f"{p}: ABI version {ver_fn()} != {ABI_VERSION} (rebuild: make -C "
+                               f"{os.path.join(PKG_ROOT, 'csrc')})")
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.dcol_abi_version() != ABI_VERSION:
-        raise DcolLibraryError(f"{p}: ABI version {lib.dcol_abi_version()} != {ABI_VERSION}")
     if path is None:
         _lib = lib
         # stop every resident pair server before interpreter teardown: Table.__del__ (which

@@ -37,9 +37,11 @@
 extern "C" {
 #endif
 
-#define DCOL_ABI_VERSION 3   /* 2: 14-slot multi-GPU record (status / iters as an int32 pair);
+#define DCOL_ABI_VERSION 4   /* 2: 14-slot multi-GPU record (status / iters as an int32 pair);
                                 3: DCOL_NO_GATHER + dcol_comm_all_gather, dcol_table_pair_plans,
-                                   dcol_table_pair_stats; dcol_shutdown */
+                                   dcol_table_pair_stats;
+                                4: dcol_plan_num_streams, dcol_shutdown, dcol_table_stop_pair_server,
+                                   dcol_table_pair_server_running, dcol_debug_pair_stamps */
 
 /* Primitive types (misc_primitive_constructor.py:4-88). */
 enum dcol_shape_type {

@@ -48,6 +48,7 @@ extern "C" int dcol_emul_batch(const dcol_shape_desc* shapes, int32_t n, int64_t
     const bool no_ball = std::getenv("DCOL_NO_BALL") != nullptr;
     const bool no_cone = std::getenv("DCOL_NO_CONE") != nullptr;
     const bool part = std::getenv("DCOL_NO_PART") == nullptr;   // read per call (tests toggle it)
+    const bool no_box = std::getenv("DCOL_NO_BOX") != nullptr;
     for (int64_t i = 0; i < B; ++i) {
         PairClass c = classify(sh[s1[i]], sh[s2[i]], false, part);
         if (c.status != DCOL_OK) {
@@ -65,10 +66,14 @@ extern "C" int dcol_emul_batch(const dcol_shape_desc* shapes, int32_t n, int64_t
         // structured-cone specialisation (N = 4, every SOC block a cone; DCOL_NO_CONE: dense)
         const bool cone = c.nsoc > 0 && c.N == 4 && sh[s1[i]].soc_kind != SOC_BALL && sh[s2[i]].soc_kind != SOC_BALL &&
                           !no_cone;
+        // box x box axis-pair rows (Solver<..., BOX>) as the GPU plans pick them (DCOL_NO_BOX:
+        // the padding-free dense rows)
+        const bool box = c.N == 4 && c.nsoc == 0 && c.omax == 12 && c.o == 12 && sh[s1[i]].boxp && sh[s2[i]].boxp &&
+                         !no_box;
         bool done = false;
 #define EMUL_CASE(NN, NS)                                                                     \
         if (c.N == NN && c.nsoc == NS)                                                        \
-            done = c.oe > 0 ? emul::solve_part<NN, NS>(c, full, ball, A, i) : emul::solve_n<NN, NS>(c, full, ball, cone, A, i);
+            done = c.oe > 0 ? emul::solve_part<NN, NS>(c, full, ball, A, i) : emul::solve_n<NN, NS>(c, full, ball, cone, box, A, i);
         EMUL_CASE(4, 0) EMUL_CASE(4, 1) EMUL_CASE(4, 2) EMUL_CASE(5, 1) EMUL_CASE(5, 2)
         EMUL_CASE(6, 1) EMUL_CASE(6, 2) EMUL_CASE(7, 2) EMUL_CASE(8, 2)
 #undef EMUL_CASE

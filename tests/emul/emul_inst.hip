@@ -7,7 +7,7 @@
 #if EMUL_PART
 template bool emul::solve_part<EMUL_N, EMUL_NS>(const dcol_host::PairClass&, bool, bool, const dcol::KArgs&, int64_t);
 #else
-template bool emul::solve_n<EMUL_N, EMUL_NS>(const dcol_host::PairClass&, bool, bool, bool, const dcol::KArgs&, int64_t);
+template bool emul::solve_n<EMUL_N, EMUL_NS>(const dcol_host::PairClass&, bool, bool, bool, bool, const dcol::KArgs&, int64_t);
 #if EMUL_NO_PART_SHAPES
 template bool emul::solve_part<EMUL_N, EMUL_NS>(const dcol_host::PairClass&, bool, bool, const dcol::KArgs&, int64_t);
 #endif

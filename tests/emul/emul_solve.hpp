@@ -11,10 +11,16 @@ using namespace dcol_host;
 // false if no compiled shape matches.  One instantiation per (N, NSOC) and row form
 // (emul_inst.hip, built once per combination by the Makefile, in parallel).
 template <int X, int XS>
-bool solve_n(const PairClass& c, bool full, bool ball, bool cone, const KArgs& A, int64_t i) {
+bool solve_n(const PairClass& c, bool full, bool ball, bool cone, bool box, const KArgs& A, int64_t i) {
 #define DCOL_EMUL(NN, NS, OM)                                                      \
     if constexpr (NN == X && NS == XS) {                                           \
         if (c.omax == OM) {                                                        \
+            if constexpr (NN == 4 && NS == 0 && OM == 12) {   /* variants.py BOX */ \
+                if (full && box) {                                                 \
+                    solve_one<NN, NS, OM, 1, true, false, false, 0, 0, false, true>(A, i, 0); \
+                    return true;                                                   \
+                }                                                                  \
+            }                                                                      \
             if constexpr (NN == 4 && NS == 0) {   /* variants.py FULL shapes */    \
                 if (full) {                                                        \
                     solve_one<NN, NS, OM, 1, true>(A, i, 0);                       \
@@ -39,7 +45,7 @@ bool solve_n(const PairClass& c, bool full, bool ball, bool cone, const KArgs& A
     }
     DCOL_SHAPES(DCOL_EMUL)
 #undef DCOL_EMUL
-    (void)c; (void)full; (void)ball; (void)cone; (void)A; (void)i;
+    (void)c; (void)full; (void)ball; (void)cone; (void)box; (void)A; (void)i;
     return false;
 }
 
@@ -66,7 +72,7 @@ bool solve_part(const PairClass& c, bool full, bool ball, const KArgs& A, int64_
 }
 
 #define EMUL_SOLVE_DECL(X, XS)                                                                              \
-    extern template bool solve_n<X, XS>(const PairClass&, bool, bool, bool, const KArgs&, int64_t);        \
+    extern template bool solve_n<X, XS>(const PairClass&, bool, bool, bool, bool, const KArgs&, int64_t);        \
     extern template bool solve_part<X, XS>(const PairClass&, bool, bool, const KArgs&, int64_t);
 EMUL_SOLVE_DECL(4, 0) EMUL_SOLVE_DECL(4, 1) EMUL_SOLVE_DECL(4, 2) EMUL_SOLVE_DECL(5, 1) EMUL_SOLVE_DECL(5, 2)
 EMUL_SOLVE_DECL(6, 1) EMUL_SOLVE_DECL(6, 2) EMUL_SOLVE_DECL(7, 2) EMUL_SOLVE_DECL(8, 2)

@@ -49,6 +49,19 @@ def test_missing_library_fails_loudly(tmp_path):
         _lib.load(str(tmp_path / "nope.so"))
 
 
+def test_stale_library_fails_with_version_error(tmp_path):
+    """A library of an older ABI (here: a stand-in exporting only dcol_abi_version() = 3,
+    none of the later entry points) is refused by its version, before any signature is
+    bound -- a DcolLibraryError naming both versions, not an AttributeError."""
+    from dcol_amd import _lib
+    src = tmp_path / "stale.c"
+    src.write_text("int dcol_abi_version(void) { return 3; }\n")
+    so = tmp_path / "libstale.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)], check=True)
+    with pytest.raises(_lib.DcolLibraryError, match=f"ABI version 3 != {_lib.ABI_VERSION}"):
+        _lib.load(str(so))
+
+
 def test_package_layout():
     for sub in ("proximity/proximity.py", "proximity/proximity_gradient.py", "primitives/misc_primitive_constructor.py",
                 "dcol_amd/_lib.py", "csrc/dcol_device.hpp", "csrc/dcol_capi.cpp"):
