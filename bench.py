@@ -76,12 +76,16 @@ def pairs(B, n_shapes, seed):
 
 
 def _oracle_chunk(args):
+    """one single-threaded worker (OMP_NUM_THREADS=1 per process): the
+    BLAS / OpenMP pools of the forked worker limited to one thread"""
     tab, s1, s2, p1, p2 = args
-    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    os.environ["OMP_NUM_THREADS"] = "1"
+    from threadpoolctl import threadpool_limits
     from oracle import dcol_oracle as O
-    t0 = time.perf_counter()
-    out = O.run_batch(tab, s1, s2, p1, p2, 1e-6, True)
-    return time.perf_counter() - t0, out["status"]
+    with threadpool_limits(limits=1):
+        t0 = time.perf_counter()
+        out = O.run_batch(tab, s1, s2, p1, p2, 1e-6, True)
+        return time.perf_counter() - t0, out["status"]
 
 
 def cpu_baseline(tab, s1, s2, p1, p2, sample, workers):
@@ -152,8 +156,12 @@ def cpu_share(requested=0):
     omp = os.environ.get("OMP_NUM_THREADS")
     share = min(avail, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else avail
     workers = max(1, min(requested, avail) if requested > 0 else share)
+    budget = ("; the GPU pool grants a one-GPU job 16 CPUs of a shared host and pins that share in "
+              "OMP_NUM_THREADS (its affinity mask and os.cpu_count() show the whole machine, whose other CPUs "
+              "belong to other jobs' GPUs) -- so `cores` is the granted budget, one single-threaded worker per "
+              "granted CPU, and `per_core` is the figure comparable across hosts") if share < avail else ""
     return workers, (f"{workers} workers; {avail} CPUs in this process's affinity mask, os.cpu_count() "
-                     f"{os.cpu_count()}, OMP_NUM_THREADS {omp or 'unset'}")
+                     f"{os.cpu_count()}, OMP_NUM_THREADS {omp or 'unset'}" + budget)
 
 
 def read_traffic(profile_dir, kernel_substr="prox_kernel"):
@@ -167,6 +175,30 @@ def read_traffic(profile_dir, kernel_substr="prox_kernel"):
         return d.get("bytes_per_launch")
     except Exception:
         return None
+
+
+def executed_fp64(kern_ms, B, flops_pair):
+    """The FP64 work the solve kernel EXECUTES, beside the counted model: from the committed
+    rocprofv3 PMC pass (profiles/pmc_fp64.json, tools/pmc_fp64.py: (ADD + MUL + 2 FMA + TRANS)
+    F64 wave-instructions x 64 per launch) over this run's kernel_ms, and the pass's VALU
+    issue fraction.  The counted model follows the reference's algorithm op by op (its FD
+    gradient re-assembles the rows 13 times, ~8.4 kflop; its NT scalings recompute J(s), J(z)),
+    which the kernel does in closed form, so it executes fewer flops per
+    pair than it is credited with: executed_frac is the hardware's FP64 utilisation."""
+    path = os.path.join(REPO, "profiles", "pmc_fp64.json")
+    if not os.path.exists(path):
+        return {}
+    try:
+        d = json.load(open(path))
+        per_pair = d["executed_flops_per_pair"]
+        tf = per_pair * B / (kern_ms * 1e-3) / 1e12
+        return {"executed_flops_per_pair": per_pair, "executed_achieved": tf,
+                "executed_frac": tf / FP64_VECTOR_PEAK_TFS, "valu_issue_frac": d["valu_issue_frac"],
+                "fp64_share_of_valu": d["fp64_share_of_valu"], "counted_over_executed": flops_pair / per_pair,
+                "executed_source": "profiles/pmc_fp64.json (rocprofv3 PMC pass of this kernel, tools/pmc_fp64.py) "
+                                   "over this run's kernel_ms"}
+    except Exception:
+        return {}
 
 
 def main():
@@ -395,7 +427,8 @@ def main():
                           "frac": flops_pair * B / (kern_ms * 1e-3) / 1e12 / FP64_VECTOR_PEAK_TFS,
                           "flops_per_pair": flops_pair,
                           "flops_source": "op-counting C restatement, profiles/flop_model.json"
-                          if os.path.exists(os.path.join(REPO, "profiles", "flop_model.json")) else "hand model"},
+                          if os.path.exists(os.path.join(REPO, "profiles", "flop_model.json")) else "hand model",
+                          **executed_fp64(kern_ms, B, flops_pair)},
         "timing": "value = pairs / ms_per_step of K steps on one stream; kernel_ms = the HIP-event time of that same "
                   "timed region on the launch stream / K (the per-launch duration of the back-to-back launches), the "
                   "rooflines' time base",
@@ -458,7 +491,9 @@ def summary(line):
     m = line.get("mixed1m") or {}
     d = line.get("dropin") or {}
     out = {"value": line["value"], "ms_per_step": line["ms_per_step"], "kernel_ms": line["kernel_ms"],
-           "fp64_frac": line["roofline_fp64"]["frac"], "hbm_frac": line["roofline"]["frac"],
+           "fp64_frac": line["roofline_fp64"]["frac"],
+           "fp64_executed_frac": line["roofline_fp64"].get("executed_frac"),
+           "valu_issue_frac": line["roofline_fp64"].get("valu_issue_frac"), "hbm_frac": line["roofline"]["frac"],
            "pipelined_value": line["pipeline"]["value"]}
     if m:
         out["mixed1m"] = {"value": m["value"], "ms_per_step": m["ms_per_step"], "kernel_ms": m.get("kernel_ms"),

@@ -232,10 +232,12 @@ struct dcol_plan {
     std::vector<int> issue;      // launch issue order (assign_lanes: longest first); empty = as built
     hipEvent_t fork = nullptr;   // recorded on the caller's stream, awaited by the side streams
     hipEvent_t join[kSideStreams] = {};
-    // fused launch (small mixed plans): one segment per solve bucket, in launch order
+    // fused launch (small mixed plans) or packed launch (mid-size plans, packed = true): one
+    // segment per solve bucket, in descending per-pair cost (plan_segments)
     std::vector<FusedSeg> segs;
     FusedSeg* d_segs = nullptr;
     int64_t fused_blocks = 0;
+    bool packed = false;
     bool fused() const { return !segs.empty(); }
     void* d_susp = nullptr;      // DCOL_PLAN_SUSPEND scratch (one allocation for every such launch)
     ~dcol_plan() {
@@ -443,6 +445,13 @@ int dcol_pair_dims(const dcol_table* t, int32_t s1, int32_t s2, int32_t* m, int3
 namespace {
 void assign_lanes(dcol_plan* p);
 
+// DCOL_SMALL_FANOUT=1: a small plan the fused kernel cannot take fans its latency-configured
+// buckets out (the behaviour before the packed launch; A/B runs)
+bool small_fanout() {
+    static const bool on = std::getenv("DCOL_SMALL_FANOUT") != nullptr;
+    return on;
+}
+
 // DCOL_NO_BALL=1: ball-SOC pairs run the dense kernels too (A/B runs, tests)
 bool ball_disabled() {
     static const bool off = std::getenv("DCOL_NO_BALL") != nullptr;
@@ -458,6 +467,17 @@ bool box_disabled() {
 bool cone_disabled() {
     static const bool off = std::getenv("DCOL_NO_CONE") != nullptr;
     return off;
+}
+
+// Lanes below which a plan counts as small -- it cannot fill the GPU: every bucket takes its
+// latency configuration and a mixed plan runs as one fused launch (bucket_pairs, plan_fuse).
+// 64 x SIMDs (one wave per SIMD); DCOL_SMALL_PLAN_LANES=<n> for A/B runs.
+int64_t small_lanes(const dcol_table* t) {
+    static const int64_t v = [] {
+        const char* e = std::getenv("DCOL_SMALL_PLAN_LANES");
+        return e ? std::atoll(e) : 0LL;
+    }();
+    return v > 0 ? v : 64LL * t->simds;
 }
 
 // A launch too small to fill the GPU runs the configuration with the shortest per-pair
@@ -497,10 +517,11 @@ void latency_config(Launch& L) {
 // is slower than the dense rows' multi-lane groups -- polygon x box, 1,000 pairs: 84 us in
 // the (11, 5) one-lane bucket against 52 us in the dense (6, 1, 12) four-lane kernel)
 // small_out: set to whether the plan cannot fill the GPU (its buckets took their latency
-// configurations)
+// configurations); force_large: bucket as a plan that fills it (throughput configurations:
+// the packed launch of a small plan the fused kernel cannot take, bucket_and_fuse)
 int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, dcol_plan* p,
                  std::vector<int32_t>& perm, bool case4, bool fused_part = false, bool lat_part = false,
-                 bool* small_out = nullptr) {
+                 bool* small_out = nullptr, bool force_large = false) {
     const int32_t ns = (int32_t)t->shapes.size();
     // kind, N, nsoc, omax, lpp, ball (SOC blocks all balls: no cone), code, oe (row partition)
     using Key = std::tuple<int, int, int, int, int, int, int, int>;
@@ -579,7 +600,7 @@ int bucket_pairs(const dcol_table* t, int64_t B, const int32_t* s1, const int32_
     int64_t plan_lanes = 0;
     for (const Group& G : groups)
         if (std::get<0>(G.key) == 0) plan_lanes += G.n * std::get<4>(G.key);
-    const bool small_plan = plan_lanes < 64LL * t->simds;
+    const bool small_plan = !force_large && plan_lanes < small_lanes(t);
     if (small_out) *small_out = small_plan;
     int64_t at = 0;
     for (auto& kv : gid_of_key) {   // key order
@@ -708,11 +729,14 @@ int plan_susp(const dcol_table* t, dcol_plan* p) {
     return DCOL_SUCCESS;
 }
 
+bool plan_segments(dcol_plan* p, int (*vid_of)(int, int, int, int, int, int));
+
 // Returns 0 when fused (or not allowed), 1 when the plan does not qualify (large or
 // single-variant), 2 when it qualifies but a bucket has no case in the fused kernel.
 int plan_fuse(const dcol_table* t, dcol_plan* p, bool allow) {
     p->segs.clear();
     p->fused_blocks = 0;
+    p->packed = false;
     if (!allow) return 0;
     int solves = 0;
     int64_t lanes = 0;
@@ -721,20 +745,76 @@ int plan_fuse(const dcol_table* t, dcol_plan* p, bool allow) {
             ++solves;
             lanes += L.n * L.lpp;
         }
-    if (solves < 2 || solves > kMaxFusedSegs || lanes >= 64LL * t->simds) return 1;
+    if (solves < 2 || solves > kMaxFusedSegs || lanes >= small_lanes(t)) return 1;
+    return plan_segments(p, fused_vid) ? 0 : 2;
+}
+
+// One segment per solve bucket with case ids from vid_of (fused_vid / packed_vid), in
+// descending per-pair cost (bucket_cost): the workgroup dispatcher hands out blocks in index
+// order as SIMDs free up, so the longest-latency waves start first and the short ones fill
+// the tail (list scheduling, longest first); DCOL_FUSED_ORDER=0: key order (A/B).  false (p
+// unchanged) when a bucket has no case.
+bool plan_segments(dcol_plan* p, int (*vid_of)(int, int, int, int, int, int)) {
+    static const bool keyorder = [] {
+        const char* e = std::getenv("DCOL_FUSED_ORDER");
+        return e && std::atoi(e) == 0;
+    }();
+    std::vector<int> order;
+    for (size_t i = 0; i < p->launches.size(); ++i)
+        if (p->launches[i].kind == 0) order.push_back((int)i);
+    if (!keyorder)
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+            const Launch& A = p->launches[a];
+            const Launch& B = p->launches[b];
+            return bucket_cost(A) / (double)A.n > bucket_cost(B) / (double)B.n;
+        });
     std::vector<FusedSeg> segs;
     int64_t block = 0;
-    for (const Launch& L : p->launches) {
-        if (L.kind != 0) continue;
-        const int vid = fused_vid(L.N, L.nsoc, L.omax, L.lpp, L.flags(), L.oe);
-        if (vid < 0) return 2;
+    for (int i : order) {
+        const Launch& L = p->launches[i];
+        const int vid = vid_of(L.N, L.nsoc, L.omax, L.lpp, L.flags(), L.oe);
+        if (vid < 0) return false;
         segs.push_back(FusedSeg{vid, L.lpp, block, L.slot0, L.n});
         block += (L.n * L.lpp + kBlock - 1) / kBlock;
     }
     p->segs = std::move(segs);
     p->fused_blocks = block;
+    p->packed = false;
     p->lanes = 1;   // no fan-out
-    return 0;
+    return true;
+}
+
+// Lanes below which a plan that is not small runs as ONE packed launch (every bucket in its
+// throughput configuration, dcol_kernels_packed.hip) instead of one launch per bucket over
+// the fan-out streams: mid-size mixed plans whose buckets each cover only part of the SIMDs
+// (a rank's shard of configs[4] at 2-8 GPUs).  16 x 64 x SIMDs (~1M lanes): measured on the
+// configs[4] shards (tools/shard_bench.py, profiles/r06_c/): packed against the fan-out
+// 0.506 / 0.549 ms at 500k pairs (775k lanes), 0.267 / 0.396 at 250k, 0.144 / 0.325 at 125k,
+// but 0.98 / 0.87 ms for the whole 1M (1.55M lanes: every bucket fills the GPU by itself and
+// its two- and three-wave kernels keep their occupancy).  DCOL_PACK_LANES=<n> for A/B runs
+// (0: never).
+int64_t pack_lanes(const dcol_table* t) {
+    static const int64_t v = [] {
+        const char* e = std::getenv("DCOL_PACK_LANES");
+        return e ? std::atoll(e) : -1LL;
+    }();
+    return v >= 0 ? v : 16LL * 64LL * t->simds;
+}
+
+// A mid-size plan (not small, below pack_lanes) with several solve buckets, every one of
+// which the packed kernel has, becomes one packed launch; otherwise p is unchanged.
+void plan_pack(const dcol_table* t, dcol_plan* p) {
+    if (p->small || p->fused()) return;
+    int solves = 0;
+    int64_t lanes = 0;
+    for (const Launch& L : p->launches)
+        if (L.kind == 0) {
+            ++solves;
+            lanes += L.n * L.lpp;
+        }
+    if (solves < 2 || solves > kMaxFusedSegs || lanes >= pack_lanes(t)) return;
+    if (!plan_segments(p, packed_vid)) return;
+    p->packed = true;
 }
 
 // bucket + fuse; a small plan whose row-partitioned buckets lack fused cases is re-bucketed
@@ -774,6 +854,30 @@ int bucket_and_fuse(const dcol_table* t, int64_t B, const int32_t* s1, const int
         p->segs.clear();
         p->fused_blocks = 0;
         assign_lanes(p);
+    }
+    if (allow_fuse) plan_pack(t, p);   // mid-size plans: one packed launch
+    // A small plan the fused kernel cannot take (a bucket without a fused case) would fan
+    // its latency-configured buckets out over the streams, one under-filled launch after
+    // another; the packed launch of its throughput configurations serves it better (one
+    // launch, every wave placed as SIMDs free) when every bucket has a
+    // packed case.  Tried on a scratch plan: p stands unless it packs.
+    if (allow_fuse && p->small && !p->fused() && !lpp_forced() && !small_fanout()) {
+        dcol_plan q;
+        std::vector<int32_t> qperm;
+        if (bucket_pairs(t, B, s1, s2, &q, qperm, case4, false, false, nullptr, true) == DCOL_SUCCESS) {
+            q.small = false;
+            plan_pack(t, &q);
+            if (q.fused()) {
+                p->launches = std::move(q.launches);
+                p->segs = std::move(q.segs);
+                p->fused_blocks = q.fused_blocks;
+                p->packed = true;
+                p->small = false;
+                p->lanes = 1;
+                p->issue.clear();
+                perm.swap(qperm);
+            }
+        }
     }
     return DCOL_SUCCESS;
 }
@@ -887,6 +991,12 @@ int dcol_plan_num_streams(const dcol_plan* p, int32_t* n) {
     return DCOL_SUCCESS;
 }
 
+int dcol_plan_launch_form(const dcol_plan* p, int32_t* form) {
+    if (!p || !form) return fail(DCOL_ERR_ARG, "dcol_plan_launch_form: NULL argument");
+    *form = !p->fused() ? DCOL_FORM_BUCKETS : (p->packed ? DCOL_FORM_PACKED : DCOL_FORM_FUSED);
+    return DCOL_SUCCESS;
+}
+
 int dcol_plan_num_buckets(const dcol_plan* p, int32_t* n) {
     if (!p || !n) return fail(DCOL_ERR_ARG, "dcol_plan_num_buckets: NULL argument");
     *n = (int32_t)p->launches.size();
@@ -948,6 +1058,8 @@ int plan_run_rec(const dcol_plan* p, const double* pose1, const double* pose2, d
     a.susp_pi = nullptr;
     a.susp_state = nullptr;
     a.susp_cap = 0;
+    // a run without envelope / implicit gradients may take a bucket's FD-only copy (LF_FDONLY)
+    const int fdonly = (flags & (DCOL_GRAD_ENVELOPE | DCOL_GRAD_IMPLICIT)) ? 0 : LF_FDONLY;
     const bool fan = p->lanes > 1 && p->fork;
     hipError_t e = hipSuccess;
     if (fan) {
@@ -977,14 +1089,15 @@ int plan_run_rec(const dcol_plan* p, const double* pose1, const double* pose2, d
             e = hipMemsetAsync(L.d_susp_count, 0, sizeof(int32_t), ls);
             if (e == hipSuccess) e = launch_susp(L.N, L.nsoc, L.omax, L.lpp, L.flags(), L.oe, b, ls);
         } else {
-            e = launch_variant(L.N, L.nsoc, L.omax, L.lpp, L.flags(), a, ls, L.oe);
+            e = launch_variant(L.N, L.nsoc, L.omax, L.lpp, L.flags() | fdonly, a, ls, L.oe);
         }
         if (e != hipSuccess) break;
     }
     if (e == hipSuccess && p->fused()) {
         a.slot0 = 0;
         a.n = 0;
-        e = launch_fused(a, p->d_segs, (int)p->segs.size(), p->fused_blocks, st);
+        e = p->packed ? launch_packed(a, p->d_segs, (int)p->segs.size(), p->fused_blocks, st)
+                      : launch_fused(a, p->d_segs, (int)p->segs.size(), p->fused_blocks, st);
     }
     if (fan) {   // join even after a failed launch, so the side streams never run ahead
         for (int l = 1; l < p->lanes; ++l) {

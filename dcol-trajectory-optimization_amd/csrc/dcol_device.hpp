@@ -2178,8 +2178,11 @@ DCOL_HD void launder(P& p) {
 // MODE 0: one launch; 1: main launch of a suspend / resume pair (KArgs susp_*); 2: the
 // resume launch, for continuation entry ci (pi = its pair)
 // GLDS: G rows in LDS (Solver; the one-wave-per-workgroup solve kernels only)
+// FDONLY: the copy built for the reference's FD gradient mode alone (launched only for runs
+// without DCOL_GRAD_ENVELOPE / DCOL_GRAD_IMPLICIT): the envelope and implicit code is not
+// compiled in, so its register pressure never shapes the FD path (variants.py BOX_FD)
 template <int N, int NSOC, int OMAX, int LPP, bool FULL = false, bool BALL = false, bool CONE = false, int OE = 0,
-          int MODE = 0, bool GLDS = false, bool BOX = false>
+          int MODE = 0, bool GLDS = false, bool BOX = false, bool FDONLY = false>
 DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1, int k1o = -1, int k2o = -1) {
     DCOL_STAMP(A, pi, q, 0);
     const int64_t B = A.B;
@@ -2247,30 +2250,33 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1, int k
         launder(L.rows);
         launder(L.pose1);
         launder(L.pose2);
-#pragma unroll
-        for (int c = 0; c < 6; ++c) {
-            th1[c] = L.pose1[c * B + pi];
-            th2[c] = L.pose2[c * B + pi];
-        }
         const DevShape& T1 = L.shapes[k1];
         const DevShape& T2 = L.shapes[k2];
         if (ok) {
-            // group sums for both primitives first (every lane of the group), then each
-            // lane differentiates one primitive: lane q takes primitive q & 1, so a 2+-lane
-            // group does the two 6-coordinate gradients side by side instead of both in
-            // every lane (a 1-lane group does both in turn)
             using Agg = typename Slv::LagAgg;
-            const Agg ag0 = P.lag_aggregate(T1, 0);
-            const Agg ag1 = P.lag_aggregate(T2, 1);
-            // implicit mode: weights a = -W^-2 G v at this iterate, aggregated like z
-            const bool imp = (A.flags & F_GRAD_IMP) != 0;
-            Agg agA0 = ag0, agA1 = ag1;
+            // implicit mode first: its weights a = -W^-2 G v at this iterate, aggregated like
+            // z -- so that nothing of the other modes (the z aggregates, the poses) is live
+            // across implicit_weights' normal matrix and Cholesky factor (held across it, they
+            // spilled to scratch in every mode: 124 B per lane in the three-wave BOX kernel)
+            const bool imp = !FDONLY && (A.flags & F_GRAD_IMP) != 0;
+            Agg agA0, agA1;
             bool imp_ok = false;
             if (imp) {
                 double wts[Slv::M];
                 imp_ok = P.implicit_weights(wts);
                 agA0 = P.lag_aggregate(T1, 0, wts);
                 agA1 = P.lag_aggregate(T2, 1, wts);
+            }
+            // group sums for both primitives first (every lane of the group), then each
+            // lane differentiates one primitive: lane q takes primitive q & 1, so a 2+-lane
+            // group does the two 6-coordinate gradients side by side instead of both in
+            // every lane (a 1-lane group does both in turn)
+            const Agg ag0 = P.lag_aggregate(T1, 0);
+            const Agg ag1 = P.lag_aggregate(T2, 1);
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                th1[c] = L.pose1[c * B + pi];
+                th2[c] = L.pose2[c * B + pi];
             }
             constexpr int NP = LPP >= 2 ? 1 : 2;
 #pragma unroll
@@ -2295,7 +2301,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1, int k
                     for (int c = 0; c < 4; ++c) agA.zs[c] = prim ? agA1.zs[c] : agA0.zs[c];
                     agA.kind = ag.kind;
                     P.imp_grad_prim(agA, ag, T, prim, th, gp);
-                } else if (A.flags & (F_GRAD_ENV | F_GRAD_IMP)) {
+                } else if (!FDONLY && (A.flags & (F_GRAD_ENV | F_GRAD_IMP))) {
                     P.env_grad_prim(ag, T, prim, th, gp);
                 } else {
                     P.fd_grad_prim(ag, T, prim, th, gp);
@@ -2360,7 +2366,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1, int k
 constexpr int kSolveBlock = DCOL_BLOCK;
 static_assert(kSolveBlock % 64 == 0, "one or more whole waves per workgroup");
 
-// FL: variant flags, bit 0 FULL, bit 1 BALL, bit 2 CONE, bit 3 BOX (variants.py)
+// FL: variant flags, bit 0 FULL, bit 1 BALL, bit 2 CONE, bit 3 BOX, bit 6 FD-only gradient (variants.py)
 // OE > 0: the row-partitioned (PART) copy with OE extra-column row slots (Solver).
 // FL bit 4 (16): the main launch of a suspend / resume pair (solve_one MODE 1)
 // WPS >= 10: the LDS-rows copy (Solver GLDS) at WPS - 10 waves per SIMD (variants.py);
@@ -2378,7 +2384,7 @@ __global__ void __launch_bounds__(kSolveBlock, WPS % 10) prox_kernel(KArgs A) {
     if (slot >= A.n) return;
     const int64_t pi = A.perm ? (int64_t)A.perm[A.slot0 + slot] : (A.slot0 + slot);
     solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0, OE, (FL & 16) ? 1 : 0,
-              kGlds && WPS >= 10, (FL & 8) != 0>(A, pi, q);
+              kGlds && WPS >= 10, (FL & 8) != 0, (FL & 64) != 0>(A, pi, q);
 }
 
 // The resume launch of a suspend / resume pair: one lane group per continuation entry;

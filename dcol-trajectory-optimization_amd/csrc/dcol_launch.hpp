@@ -5,7 +5,7 @@
 
 namespace dcol {
 // launch flags of a bucket (the variant flags FL of variants.py a launch may use)
-enum : int { LF_FULL = 1, LF_BALL = 2, LF_CONE = 4, LF_BOX = 8 };
+enum : int { LF_FULL = 1, LF_BALL = 2, LF_CONE = 4, LF_BOX = 8, LF_FDONLY = 64 };   // (LF_FDONLY: a run without envelope / implicit gradients)
 constexpr int kBlock = kSolveBlock;   // threads per workgroup of the solve kernel
 constexpr int kSideStreams = 7;   // capacity of the extra streams for concurrent variant launches
                                   // (dcol_capi.cpp side_streams(): 3 by default, DCOL_SIDE_STREAMS)
@@ -36,6 +36,10 @@ hipError_t launch_susp(int N, int nsoc, int omax, int lpp, int flags, int oe, co
 // the fused kernel lacks it
 int fused_vid(int N, int nsoc, int omax, int lpp, int flags, int oe = 0);
 hipError_t launch_fused(const KArgs& args, const FusedSeg* d_segs, int nseg, int64_t blocks, hipStream_t stream);
+// packed multi-bucket launch (dcol_kernels_packed.hip): a mid-size plan's buckets in their
+// throughput configurations in ONE launch (segments as FusedSeg, vid = packed case id)
+int packed_vid(int N, int nsoc, int omax, int lpp, int flags, int oe = 0);
+hipError_t launch_packed(const KArgs& args, const FusedSeg* d_segs, int nseg, int64_t blocks, hipStream_t stream);
 
 // Mailbox of the one-pair server (dcol_prox_pair; dcol_kernels_server.hip prox_pair_server):
 // device-mapped pinned host memory, one per table.  The caller writes the poses and the
@@ -84,7 +88,7 @@ hipError_t launch_pair_server(const KArgs& args, PairBox* box, int64_t idle_tick
         if (reset) (void)hipMemcpyToSymbol(HIP_SYMBOL(dcol_exec_violations), &z, sizeof(z));   \
         return v;                                                                              \
     }
-#define DCOL_EXEC_TAGS(X) X(n4) X(n5) X(n6) X(n7) X(n8) X(fused) X(p51) X(p52) X(p61) X(p62) X(p62d) X(susp) X(server)
+#define DCOL_EXEC_TAGS(X) X(n4) X(n5) X(n6) X(n7) X(n8) X(fused) X(packed) X(p51) X(p52) X(p61) X(p62) X(p62d) X(susp) X(server)
 #define DCOL_EXEC_DECL(tag) unsigned long long exec_violations_##tag(bool reset);
 DCOL_EXEC_TAGS(DCOL_EXEC_DECL)
 DCOL_EXEC_DECL(capi)   // the C-ABI unit's own counter (dcol_debug_exec_selftest)

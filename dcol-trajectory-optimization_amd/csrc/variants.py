@@ -40,6 +40,7 @@ Generates dcol_variants.inc (FL = variant flags: bit 0 FULL, bit 1 BALL, bit 2 C
   DCOL_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, 0) for every compiled kernel
   DCOL_FULL_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, 1) for the padding-free copies
   DCOL_BOX_VARIANTS(X)   X(N, NSOC, OMAX, LPP, WPS, 9) for the box x box axis-pair copies
+  DCOL_BOX_FD_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, 73) their FD-only-gradient copies
   DCOL_BALL_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, 2) for the ball-SOC copies
   DCOL_CONE_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, 4) for the structured-cone copies
   DCOL_SHAPES(X)    X(N, NSOC, OMAX) once per shape (used by the test emulator)
@@ -48,6 +49,7 @@ Generates dcol_variants.inc (FL = variant flags: bit 0 FULL, bit 1 BALL, bit 2 C
   DCOL_PART_SHAPES(X)    X(N, NSOC, OMAX, OE) once per PART bucket (host bucketing, emulator)
   DCOL_FUSED_PART_VARIANTS(X)  X(ID, N, NSOC, OMAX, LPP, FL, OE) the PART cases of the fused kernel
   DCOL_SUSP_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, FL, OE) suspend / resume copies (FL bit 4 = 16)
+  DCOL_PACKED_VARIANTS(X)  X(ID, N, NSOC, OMAX, LPP, FL, OE) the cases of the packed kernel
 
 SUSP variants (dcol_device.hpp KArgs susp_*, dcol_kernels_susp.hip): a large launch runs as a
 main launch in which a wave hands its last few iterating pairs (<= DCOL_SUSPEND_T of 32, after
@@ -129,6 +131,10 @@ FULL = {(4, 0)}   # shapes with padding-free copies (see module docstring)
 # -- 24 scratch accesses per loop, 87 us per 100k; one lane per pair with LDS rows at two
 # waves (4, 0, 12, 1, 12) -- spill-free, 64.5 us per 100k, 2.54e9 at 1M
 BOX = [(4, 0, 12, 2, 3)]
+# FD-only copies of the BOX kernel (FL 73 = FULL | BOX | 64): launched for runs whose gradient
+# mode is the reference's FD (or none) -- the headline -- without the envelope / implicit
+# code, whose register pressure at 168 VGPRs spilled 124 B per lane to scratch in every mode
+BOX_FD = BOX
 # padding-free copies of the structured-cone kernels: (N, NSOC, OMAX) whose pairs commonly
 # fill the bucket (cone x box: the cone's base row + 6 faces = 7)
 FULL_CONE = {(4, 1, 7)}
@@ -269,6 +275,50 @@ def fused():
     return out
 
 
+# PACKED variants (dcol_kernels_packed.hip): one launch for a whole mid-size plan -- more
+# lanes than a small plan (whose buckets take their latency configurations and the fused
+# kernel) but too few for every bucket to fill the GPU by itself (a rank's shard of a mixed
+# batch: 125k-250k pairs over ~15 buckets of 8-17k pairs; round-6 measurement: each bucket
+# 20-80 us of single-wave latency on 15-30 % of the SIMDs, three in flight -> 0.32 ms per
+# 125k step).  Its workgroups switch on a per-segment case id like the fused kernel's, but
+# each case is a bucket's THROUGHPUT configuration (the first (LPP, WPS) of its flavour, the
+# per-variant kernels' own), and the kernel runs one wave per SIMD with the register rows
+# (GLDS off: it has the registers), so the workgroup dispatcher packs every bucket's waves
+# onto free SIMDs in segment order.  Cases: the dense shapes and PART buckets up to
+# PACK_OMAX rows, every flavour, listed per shape in the per-N launchers' preference order
+# (BOX, FULL_CONE, FULL, BALL, CONE, plain; PART: FULL|BALL, BALL, FULL, dense).
+PACK_OMAX = 12
+
+
+def packed():
+    out = []
+    box = {(n, s, o): l for n, s, o, l, _ in BOX}
+    for (n, s), os_ in sorted(OMAX.items()):
+        if n > 6:
+            continue
+        for o in os_:
+            if o > PACK_OMAX:
+                continue
+            if (n, s, o) in box:
+                out.append((n, s, o, box[(n, s, o)], 9, 0))
+            if (n, s, o) in FULL_CONE:
+                out.append((n, s, o, configs_fl(n, s, o, 4)[0][0], 5, 0))
+            if (n, s) in FULL:
+                out.append((n, s, o, configs(n, s, o)[0][0], 1, 0))
+            if ball(n, s) and (n, s, o, configs_fl(n, s, o, 2)[0][0]) not in BALL_SKIP:
+                out.append((n, s, o, configs_fl(n, s, o, 2)[0][0], 2, 0))
+            if cone(n, s, o):
+                out.append((n, s, o, configs_fl(n, s, o, 4)[0][0], 4, 0))
+            out.append((n, s, o, configs(n, s, o)[0][0], 0, 0))
+    for (n, s), bl in sorted(PART.items()):
+        for (o, oe) in sorted(bl):
+            if o > PACK_OMAX:
+                continue
+            for fl in part_flavours(n, s):
+                out.append((n, s, o, part_configs(n, s, o, oe, fl)[0][0], fl, oe))
+    return out
+
+
 def main():
     here = os.path.dirname(os.path.abspath(__file__))
     shapes = [(n, s, o) for (n, s), os_ in sorted(OMAX.items()) for o in os_]
@@ -278,6 +328,8 @@ def main():
     lines += [f"    X({n}, {s}, {o}, {l}, {w}, 1) \\" for n, s, o in shapes if (n, s) in FULL for l, w in configs(n, s, o)]
     lines += ["", "#define DCOL_BOX_VARIANTS(X) \\"]
     lines += [f"    X({n}, {s}, {o}, {l}, {w}, 9) \\" for n, s, o, l, w in BOX]
+    lines += ["", "#define DCOL_BOX_FD_VARIANTS(X) \\"]
+    lines += [f"    X({n}, {s}, {o}, {l}, {w}, 73) \\" for n, s, o, l, w in BOX_FD]
     lines += ["", "#define DCOL_FULL_CONE_VARIANTS(X) \\"]
     lines += [f"    X({n}, {s}, {o}, {l}, {w}, 5) \\" for n, s, o in shapes if (n, s, o) in FULL_CONE
               for l, w in configs_fl(n, s, o, 4)]
@@ -298,6 +350,8 @@ def main():
     lines += ["", "#define DCOL_FUSED_PART_VARIANTS(X) \\"]
     base = len(fused())
     lines += [f"    X({base + i}, {n}, {s}, {o}, {l}, {f}, {oe}) \\" for i, (n, s, o, l, f, oe) in enumerate(fused_part())]
+    lines += ["", "#define DCOL_PACKED_VARIANTS(X) \\"]
+    lines += [f"    X({i}, {n}, {s}, {o}, {l}, {fl}, {oe}) \\" for i, (n, s, o, l, fl, oe) in enumerate(packed())]
     lines += ["", "#define DCOL_SUSP_VARIANTS(X) \\"]
     lines += [f"    X({n}, {s}, {o}, {l}, {w}, {fl | 16}, {oe}) \\" for n, s, o, l, w, fl, oe in SUSP]
     lines.append("")

@@ -54,6 +54,7 @@ SIGNATURES = {
     "dcol_plan_destroy": (c_int, [c_void_p]),
     "dcol_plan_num_launches": (c_int, [c_void_p, POINTER(c_int32)]),
     "dcol_plan_num_streams": (c_int, [c_void_p, POINTER(c_int32)]),
+    "dcol_plan_launch_form": (c_int, [c_void_p, POINTER(c_int32)]),
     "dcol_plan_num_buckets": (c_int, [c_void_p, POINTER(c_int32)]),
     "dcol_plan_bucket": (c_int, [c_void_p, c_int32, POINTER(c_int32), POINTER(c_int64)]),
     "dcol_plan_suspended": (c_int, [c_void_p, POINTER(c_int64)]),

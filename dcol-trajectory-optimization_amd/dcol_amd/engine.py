@@ -132,6 +132,10 @@ class Plan:
         self.num_buckets = int(n.value)        # variant buckets (incl. rejected pairs)
         _lib.check(lib.dcol_plan_num_streams(h, ctypes.byref(n)), "dcol_plan_num_streams")
         self.num_streams = int(n.value)        # streams a run's launches are spread over
+        _lib.check(lib.dcol_plan_launch_form(h, ctypes.byref(n)), "dcol_plan_launch_form")
+        # how a run launches its buckets: "buckets" (one launch each), "fused" (small plan),
+        # "packed" (mid-size plan; include/dcol.h enum dcol_plan_form)
+        self.launch_form = ("buckets", "fused", "packed")[int(n.value)]
 
     def buckets(self) -> list:
         """The plan's variant buckets (dcol_plan_bucket): one dict per bucket with kind

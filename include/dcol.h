@@ -40,8 +40,9 @@ extern "C" {
 #define DCOL_ABI_VERSION 4   /* 2: 14-slot multi-GPU record (status / iters as an int32 pair);
                                 3: DCOL_NO_GATHER + dcol_comm_all_gather, dcol_table_pair_plans,
                                    dcol_table_pair_stats;
-                                4: dcol_plan_num_streams, dcol_shutdown, dcol_table_stop_pair_server,
-                                   dcol_table_pair_server_running, dcol_debug_pair_stamps */
+                                4: dcol_plan_num_streams, dcol_plan_launch_form, dcol_shutdown,
+                                   dcol_table_stop_pair_server, dcol_table_pair_server_running,
+                                   dcol_debug_pair_stamps */
 
 /* Primitive types (misc_primitive_constructor.py:4-88). */
 enum dcol_shape_type {
@@ -157,6 +158,12 @@ int dcol_plan_num_launches(const dcol_plan* plan, int32_t* n); /* kernel launche
 int dcol_plan_num_streams(const dcol_plan* plan, int32_t* n); /* streams a run spreads its launches over:
                                                                   the caller's + side streams (1 = caller's only) */
 int dcol_plan_num_buckets(const dcol_plan* plan, int32_t* n);  /* variant buckets (incl. rejects) */
+/* How a run launches its solve buckets: DCOL_FORM_BUCKETS one launch per bucket (over
+ * dcol_plan_num_streams streams), DCOL_FORM_FUSED one fused launch (a small plan: latency
+ * configurations), DCOL_FORM_PACKED one packed launch (a mid-size plan: throughput
+ * configurations).                                                   */
+enum dcol_plan_form { DCOL_FORM_BUCKETS = 0, DCOL_FORM_FUSED = 1, DCOL_FORM_PACKED = 2 };
+int dcol_plan_launch_form(const dcol_plan* plan, int32_t* form);
 /* Bucket i (0 <= i < dcol_plan_num_buckets) of a plan, for tests and tools: info[0] kind (0 a
  * solve bucket, 1 rejected pairs), [1] N (primal columns), [2] SOC blocks, [3] orthant-row
  * bucket OMAX, [4] lanes per pair the launch runs at, [5] extra-column slots of a row-

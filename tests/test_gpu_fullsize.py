@@ -181,8 +181,13 @@ eng = Engine(device=0)
 ids = np.array([eng.register(spec_from_arrays(tab, k)) for k in range(len(tab["type"]))], np.int32)
 r = eng.solve_host(ids[s1], ids[s2], p1, p2, grad="fd", contact=True)
 r2 = eng.solve_host(ids[s1[:100000]], ids[s2[:100000]], p1[:100000], p2[:100000], grad="envelope", contact=False)
+# a rank's shard at world 8 (125k pairs): the packed launch (dcol_kernels_packed.hip)
+from dcol_amd.dist import shard_indices
+m = shard_indices(len(s1), 0, 8, tab["type"][s1] * 8 + tab["type"][s2])
+assert eng.plan(ids[s1[m]], ids[s2[m]], cache=False).launch_form == "packed"
+r3 = eng.solve_host(ids[s1[m]], ids[s2[m]], p1[m], p2[m], grad="fd", contact=True)
 np.savez(sys.argv[1], alpha=r.alpha, grad=r.grad, contact=r.contact, iters=r.iters, status=r.status,
-         genv=r2.grad)
+         genv=r2.grad, palpha=r3.alpha, pgrad=r3.grad, pcontact=r3.contact, piters=r3.iters, pstatus=r3.status)
 """
 
 
@@ -201,9 +206,9 @@ def _mixed_outputs(tmp_path, name, lib=None, env_extra=None):
 
 
 def _assert_bitwise(a, b):
-    for k in ("status", "iters"):
+    for k in ("status", "iters", "pstatus", "piters"):
         np.testing.assert_array_equal(a[k], b[k])
-    for k in ("alpha", "grad", "contact", "genv"):
+    for k in ("alpha", "grad", "contact", "genv", "palpha", "pgrad", "pcontact"):
         same = (a[k] == b[k]) | (np.isnan(a[k]) & np.isnan(b[k]))
         assert same.all(), (k, int((~same).sum()))
 

@@ -95,24 +95,74 @@ def test_bucket_index_checked(engine):
 
 
 def test_fanout_width_by_plan_size(engine):
-    """A mixed plan that fills the GPU spreads its buckets over the caller's stream + 2 side
-    streams (three buckets in flight: DESIGN.md section 5, "Two side streams"); a small one,
-    whose buckets run their latency configurations, over the caller's + 3; a fused small plan
-    and a one-bucket plan run on the caller's stream alone."""
+    """How a mixed plan launches, by size: the whole 1M configs[4] plan
+    (every bucket fills the GPU by itself) one launch per bucket over the caller's stream + 2
+    side streams (three buckets in flight); a mid-size one (150k pairs: a rank's shard at 4-8
+    GPUs) one packed launch; a small one with fusing disallowed its latency-configured buckets
+    over the caller's + 3; a small one otherwise one fused (or, without fused cases, packed)
+    launch; a one-bucket plan the caller's stream alone."""
     import os
     import bench
-    if os.environ.get("DCOL_SIDE_STREAMS") or os.environ.get("DCOL_SIDE_STREAMS_LARGE") or os.environ.get("DCOL_NO_FANOUT"):
-        pytest.skip("fan-out width overridden by the environment")
+    if any(os.environ.get(k) for k in ("DCOL_SIDE_STREAMS", "DCOL_SIDE_STREAMS_LARGE", "DCOL_NO_FANOUT",
+                                      "DCOL_PACK_LANES", "DCOL_SMALL_FANOUT")):
+        pytest.skip("plan policy overridden by the environment")
     tab = bench.mixed_table()
     ids = _ids(engine, tab)
-    s1, s2 = bench.mixed_pairs(tab, 150_000, seed=3)[:2]
+    s1, s2 = bench.mixed_pairs(tab, 1_000_000, seed=3)[:2]
     big = engine.plan(ids[s1], ids[s2], cache=False)
-    assert len(_solves(big)) > 4 and big.num_streams == 3
+    assert len(_solves(big)) > 4 and big.num_streams == 3 and big.launch_form == "buckets"
+    mid = engine.plan(ids[s1[:150_000]], ids[s2[:150_000]], cache=False)
+    assert len(_solves(mid)) > 4 and mid.launch_form == "packed" and mid.num_streams == 1 and mid.num_launches == 1
+    # the packed plan's buckets are the throughput configurations of the large plan's
+    key = lambda b: (b["N"], b["nsoc"], b["omax"], b["lpp"], b["oe"], b["flags"])  # noqa: E731
+    assert {key(b) for b in _solves(mid)} <= {key(b) for b in _solves(big)}
     small = engine.plan(ids[s1[:2000]], ids[s2[:2000]], cache=False, fuse=False)
-    assert len(_solves(small)) > 4 and small.num_streams == 4
-    fused = engine.plan(ids[s1[:2000]], ids[s2[:2000]], cache=False)
-    assert fused.num_streams == (1 if fused.num_launches == 1 else 4)
+    assert len(_solves(small)) > 4 and small.num_streams == 4 and small.launch_form == "buckets"
+    one = engine.plan(ids[s1[:2000]], ids[s2[:2000]], cache=False)
+    assert one.launch_form in ("fused", "packed") and one.num_streams == 1 and one.num_launches == 1
     tb = bench.shape_table(64, 0)
     idb = _ids(engine, tb)
     b1, b2 = bench.pairs(100_000, 64, 0)[:2]
-    assert engine.plan(idb[b1], idb[b2], cache=False).num_streams == 1
+    p1 = engine.plan(idb[b1], idb[b2], cache=False)
+    assert p1.num_streams == 1 and p1.launch_form == "buckets"
+
+
+@pytest.mark.parametrize("world", [8, 32])
+def test_packed_launch_bitwise_equal_to_bucket_launches(engine, world):
+    """The packed launch (dcol_kernels_packed.hip: every bucket of a mid-size plan in one
+    launch, each in its throughput configuration, segments longest first) runs the same
+    solver copies as the per-bucket kernels: rank 0's class-balanced shard of the configs[4]
+    batch at world 8 (125k pairs) and 32 (31k: a small plan the fused kernel cannot take,
+    packed instead of fanned out) gives BITWISE the outputs of the same buckets launched one
+    by one (fuse=False), and of the shard's pairs inside the whole 1M plan."""
+    import torch
+    import bench
+    from dcol_amd import alloc_outputs
+    from dcol_amd.dist import shard_indices
+    tab = bench.mixed_table()
+    ids = _ids(engine, tab)
+    B = 1_000_000
+    s1, s2, p1, p2 = bench.mixed_pairs(tab, B, seed=0)
+    mine = shard_indices(B, 0, world, tab["type"][s1] * 8 + tab["type"][s2])
+    dev = torch.device("cuda", engine.device)
+    d1 = torch.from_numpy(np.ascontiguousarray(p1[mine].T)).to(dev)
+    d2 = torch.from_numpy(np.ascontiguousarray(p2[mine].T)).to(dev)
+    packed = engine.plan(ids[s1[mine]], ids[s2[mine]], cache=False)
+    assert packed.launch_form == "packed" and packed.num_launches == 1
+    apart = engine.plan(ids[s1[mine]], ids[s2[mine]], cache=False, fuse=False)
+    assert apart.launch_form == "buckets"
+    a = packed.run(d1, d2, grad="fd", contact=True)
+    b = apart.run(d1, d2, grad="fd", contact=True)
+    torch.cuda.synchronize()
+    for k in ("status", "iters", "alpha", "grad", "contact"):
+        assert torch.equal(a[k], b[k]), k
+    if world == 8:   # against the whole batch's plan (one launch per bucket, throughput configurations)
+        whole = engine.plan(ids[s1], ids[s2], cache=False)
+        w1 = torch.from_numpy(np.ascontiguousarray(p1.T)).to(dev)
+        w2 = torch.from_numpy(np.ascontiguousarray(p2.T)).to(dev)
+        out = alloc_outputs(B, dev, want_grad=True, want_contact=False)
+        whole.run(w1, w2, grad="fd", contact=False, out=out)
+        sel = torch.from_numpy(mine).to(dev)
+        for k in ("status", "iters", "alpha"):
+            assert torch.equal(out[k][sel], a[k]), k
+        assert torch.equal(out["grad"][:, sel], a["grad"])
