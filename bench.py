@@ -229,6 +229,11 @@ def main():
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo for rehearsals)")
     ap.add_argument("--mixed-steps", type=int, default=20,
                     help="timed steps of the configs[4] sub-measurement (mixed1m) of the default line; 0 = skip")
+    ap.add_argument("--shard-steps", type=int, default=30,
+                    help="mixed1m at world 1: timed steps per shard of the configs[4] per-rank regime (`shards`: rank "
+                         "0's class-balanced shard at world N solved alone on this GPU); 0 = skip")
+    ap.add_argument("--shard-worlds", default="2,3,4,6,8,16,32,64,128,512,4096",
+                    help="the world sizes N of the `shards` section (shard = 1M / N pairs)")
     ap.add_argument("--torch-gather", action="store_true",
                     help="mixed1m: all-gather through torch.distributed instead of the C-ABI RCCL path")
     ap.add_argument("--hw-queues", type=int, default=8,
@@ -499,6 +504,10 @@ def summary(line):
         out["mixed1m"] = {"value": m["value"], "ms_per_step": m["ms_per_step"], "kernel_ms": m.get("kernel_ms"),
                           "fp64_frac": (m.get("roofline_fp64") or {}).get("frac"),
                           "pipelined_value": m["pipeline"]["value"]}
+    sh = m.get("shards") if m else None
+    if sh:
+        out["mixed1m"]["shards_solve_ms"] = {str(r["world"]): r["solve_ms"] for r in sh["per_world"] if r["world"] in (1, 2, 4, 8)}
+        out["mixed1m"]["crossover_pairs"] = sh["crossover_pairs"]
     if "kernel_1m" in line:
         out["kernel_1m"] = {"pair_solves_per_s": line["kernel_1m"]["pair_solves_per_s"],
                             "fp64_frac": line["kernel_1m"]["roofline_fp64"]["frac"]}
@@ -1017,6 +1026,8 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup, 
                                  "flops_per_pair": flops_local / max(n, 1),
                                  "note": "rank 0's shard: counted per-class flops (profiles/flop_model.json) at each "
                                          "pair's iteration count / its solve time in the timed run (kernel_ms)"}
+    if world == 1 and B == 1_000_000 and args.shard_steps > 0:
+        line["shards"] = shards_section(args, eng, ids, tab, s1, s2, p1, p2, cost, dev)
     if args.check:
         from oracle import c_oracle
         k = min(args.check * 8, B)
@@ -1029,6 +1040,70 @@ def mixed_measure(args, world, rank, local, dev, coll_dev, dist, steps, warmup, 
                                    <= 1e-5 * np.maximum(np.abs(ref["grad"][ok]).max(1), 1)))
             if args.grad == "fd" else None}   # the C oracle restates the reference's FD gradient only
     return line
+
+
+def shards_section(args, eng, ids, tab, s1, s2, p1, p2, cost, dev):
+    """configs[4]'s per-rank regime, measured on this one GPU: for each N of --shard-worlds,
+    rank 0's class-balanced shard (dcol_amd.dist.shard_indices: the shard bench.py --gpus N
+    gives rank 0) solved alone -- K steps back to back on one stream, HIP events around the
+    region, the library's plan policy (a packed launch for mid-size plans, DESIGN.md section
+    5) -- with its FP64 fraction and its ratio to linear ((1M solve) / N); the all-gather of
+    the N-rank step MODELLED (dcol_amd.dist.gather_ms: no multi-GPU node in this pool) and the
+    projected strong-scaling step = shard solve + all-gather; B*, the smallest batch for which
+    N GPUs beat one, from this run's solve curve."""
+    import torch
+    from dcol_amd import alloc_outputs
+    from dcol_amd import dist as D
+    B = len(s1)
+    stream = torch.cuda.current_stream(dev)
+    worlds = [1] + [int(w) for w in args.shard_worlds.split(",") if int(w) > 1]
+    rows, curve = [], []
+    for N in worlds:
+        mine = D.shard_indices(B, 0, N, cost)
+        plan = eng.plan(ids[s1[mine]], ids[s2[mine]], cache=False)
+        d1 = torch.from_numpy(np.ascontiguousarray(p1[mine].T)).to(dev)
+        d2 = torch.from_numpy(np.ascontiguousarray(p2[mine].T)).to(dev)
+        out = alloc_outputs(len(mine), dev, want_grad=True, want_contact=False)
+        run = plan.bind(d1, d2, out, grad=args.grad, contact=False, stream=stream)
+        for _ in range(5):
+            run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.shard_steps):
+            run()
+        e1.record(stream)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / args.shard_steps
+        st, it = out["status"].cpu().numpy(), out["iters"].cpu().numpy()
+        fl = mixed_flops(tab, s1[mine], s2[mine], it, st, args.grad)
+        r = {"world": N, "pairs": int(len(mine)), "solve_ms": ms, "pair_solves_per_s": len(mine) / (ms * 1e-3),
+             "launch_form": plan.launch_form, "launches": plan.num_launches, "buckets": plan.num_buckets}
+        if fl is not None:
+            r["fp64_frac"] = fl / (ms * 1e-3) / 1e12 / FP64_VECTOR_PEAK_TFS
+        curve.append((len(mine), ms))
+        rows.append(r)
+        del plan, d1, d2, out, run
+    full = rows[0]["solve_ms"]
+    for r in rows[1:]:
+        N = r["world"]
+        r["linear_frac"] = full / N / r["solve_ms"]
+        g, gi = D.gather_ms(B, N), D.gather_ms(B, N, D.GATHER_IDEAL_GBPS)
+        r["gather_model"] = {"bytes_received_per_rank": int((N - 1) * -(-B // N) * D.REC * 8), "ms": g,
+                             "ms_at_ideal_xgmi": gi}
+        r["projected_step_ms"] = r["solve_ms"] + g
+        r["projected_pair_solves_per_s"] = B / ((r["solve_ms"] + g) * 1e-3)
+        r["projected_pair_solves_per_s_ideal_xgmi"] = B / ((r["solve_ms"] + gi) * 1e-3)
+    return {"note": "rank 0's class-balanced shard of the 1M configs[4] batch at world N, solved alone on this GPU "
+                    f"({args.shard_steps} steps back to back on one stream, HIP events); linear_frac = (the 1M solve / N) "
+                    "/ the shard's solve; gather_model: the N-rank step's all-gather MODELLED (not measured: no "
+                    f"multi-GPU node here) at {D.GATHER_BUS_GBPS:.0f} GB/s RCCL bus bandwidth + {D.GATHER_LAT_MS} ms, "
+                    f"and at the {D.GATHER_IDEAL_GBPS:.0f} GB/s xGMI ingress bound; projected_step = shard solve + modelled "
+                    "all-gather (the bench's serial mixed1m step)",
+            "solve_ms_1m": full, "per_world": rows,
+            "crossover_pairs": {str(N): D.shard_crossover(N, curve) for N in (2, 4, 8)},
+            "crossover_pairs_ideal_xgmi": {str(N): D.shard_crossover(N, curve, D.GATHER_IDEAL_GBPS) for N in (2, 4, 8)},
+            "crossover_note": "B*: the smallest batch for which N GPUs (shards + one all-gather) beat one GPU, from this "
+                              "run's solve curve (dcol_amd.dist.shard_crossover / should_shard)"}
 
 
 def mixed_flops(tab, s1, s2, iters, status, grad="fd"):

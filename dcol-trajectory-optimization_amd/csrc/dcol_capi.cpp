@@ -817,11 +817,6 @@ void plan_pack(const dcol_table* t, dcol_plan* p) {
     p->packed = true;
 }
 
-// bucket + fuse; a small plan whose row-partitioned buckets lack fused cases is re-bucketed
-// with those pairs on the dense-row kernels, so it keeps its single launch (latency-bound
-// plans lose far more to a fan-out than the partition saves)
-// (the buckets do not depend on allow_fuse: a DCOL_PLAN_NO_FUSE plan launches the same
-// buckets one by one)
 int bucket_and_fuse(const dcol_table* t, int64_t B, const int32_t* s1, const int32_t* s2, dcol_plan* p,
                     std::vector<int32_t>& perm, bool case4, bool allow_fuse) {
     bool small = false;
@@ -873,7 +868,7 @@ int bucket_and_fuse(const dcol_table* t, int64_t B, const int32_t* s1, const int
                 p->fused_blocks = q.fused_blocks;
                 p->packed = true;
                 p->small = false;
-                p->lanes = 1;
+                p->lanes = q.lanes;
                 p->issue.clear();
                 perm.swap(qperm);
             }
@@ -1024,7 +1019,11 @@ int plan_run_rec(const dcol_plan* p, const double* pose1, const double* pose2, d
                  int32_t flags, double* alpha, double* contact, double* grad, int32_t* iters, int32_t* status,
                  double* rec, void* stream, bool yield = true) {
     if (!p) return fail(DCOL_ERR_ARG, "dcol_plan_run: NULL plan");
-    if (yield && !p->small) yield_pair_servers(p->table->device);   // (the pair call's own launch path keeps it)
+    // (the pair call's own launch path keeps it).  A small plan keeps it too -- unless it is
+    // launched on the null stream: the server runs on a blocking stream (CU-masked streams
+    // have no non-blocking form), so null-stream work waits for it to leave, i.e. for its idle
+    // time (DCOL_PAIR_SERVER_IDLE_US) -- asking it to leave now costs a restart instead.
+    if (yield && (!p->small || stream == nullptr)) yield_pair_servers(p->table->device);
     if (p->B == 0) return DCOL_SUCCESS;
     if (!pose1 || !pose2 || (!alpha && !rec))
         return fail(DCOL_ERR_ARG, "dcol_plan_run: pose1, pose2 and alpha are required");
@@ -1033,6 +1032,9 @@ int plan_run_rec(const dcol_plan* p, const double* pose1, const double* pose2, d
     if (max_iter < 0) return fail(DCOL_ERR_ARG, "dcol_plan_run: max_iter < 0");
     const dcol_table* t = p->table;
     DeviceGuard g(t->device);
+    // the launch checks below read the thread's last HIP error: clear one a caller's earlier
+    // HIP call left behind (not ours to report)
+    (void)hipGetLastError();
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     KArgs a;
     a.shapes = t->d_shapes;

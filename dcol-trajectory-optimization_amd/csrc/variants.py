@@ -291,8 +291,15 @@ PACK_OMAX = 12
 
 
 def packed():
+    """(N, NSOC, OMAX, LPP, FL, OE) per packed case.  (One kernel at one wave per SIMD for every
+    case: a split into a one-wave and a two-wave kernel side by side on two streams measured
+    slower up to 250k pairs -- 125k 0.144 -> 0.161 ms, 62.5k 0.099 -> 0.111 -- and equal at
+    500k: the two kernels' waves compete for the same SIMDs (profiles/r06_f/).)"""
     out = []
-    box = {(n, s, o): l for n, s, o, l, _ in BOX}
+
+    def fam(w):
+        return 0
+    box = {(n, s, o): (l, w) for n, s, o, l, w in BOX}
     for (n, s), os_ in sorted(OMAX.items()):
         if n > 6:
             continue
@@ -300,22 +307,29 @@ def packed():
             if o > PACK_OMAX:
                 continue
             if (n, s, o) in box:
-                out.append((n, s, o, box[(n, s, o)], 9, 0))
+                l, w = box[(n, s, o)]
+                out.append((n, s, o, l, 9, 0, fam(w)))
             if (n, s, o) in FULL_CONE:
-                out.append((n, s, o, configs_fl(n, s, o, 4)[0][0], 5, 0))
+                l, w = configs_fl(n, s, o, 4)[0]
+                out.append((n, s, o, l, 5, 0, fam(w)))
             if (n, s) in FULL:
-                out.append((n, s, o, configs(n, s, o)[0][0], 1, 0))
+                l, w = configs(n, s, o)[0]
+                out.append((n, s, o, l, 1, 0, fam(w)))
             if ball(n, s) and (n, s, o, configs_fl(n, s, o, 2)[0][0]) not in BALL_SKIP:
-                out.append((n, s, o, configs_fl(n, s, o, 2)[0][0], 2, 0))
+                l, w = configs_fl(n, s, o, 2)[0]
+                out.append((n, s, o, l, 2, 0, fam(w)))
             if cone(n, s, o):
-                out.append((n, s, o, configs_fl(n, s, o, 4)[0][0], 4, 0))
-            out.append((n, s, o, configs(n, s, o)[0][0], 0, 0))
+                l, w = configs_fl(n, s, o, 4)[0]
+                out.append((n, s, o, l, 4, 0, fam(w)))
+            l, w = configs(n, s, o)[0]
+            out.append((n, s, o, l, 0, 0, fam(w)))
     for (n, s), bl in sorted(PART.items()):
         for (o, oe) in sorted(bl):
             if o > PACK_OMAX:
                 continue
             for fl in part_flavours(n, s):
-                out.append((n, s, o, part_configs(n, s, o, oe, fl)[0][0], fl, oe))
+                l, w = part_configs(n, s, o, oe, fl)[0]
+                out.append((n, s, o, l, fl, oe, fam(w)))
     return out
 
 
@@ -351,7 +365,7 @@ def main():
     base = len(fused())
     lines += [f"    X({base + i}, {n}, {s}, {o}, {l}, {f}, {oe}) \\" for i, (n, s, o, l, f, oe) in enumerate(fused_part())]
     lines += ["", "#define DCOL_PACKED_VARIANTS(X) \\"]
-    lines += [f"    X({i}, {n}, {s}, {o}, {l}, {fl}, {oe}) \\" for i, (n, s, o, l, fl, oe) in enumerate(packed())]
+    lines += [f"    X({i}, {n}, {s}, {o}, {l}, {fl}, {oe}) \\" for i, (n, s, o, l, fl, oe, _) in enumerate(packed())]
     lines += ["", "#define DCOL_SUSP_VARIANTS(X) \\"]
     lines += [f"    X({n}, {s}, {o}, {l}, {w}, {fl | 16}, {oe}) \\" for n, s, o, l, w, fl, oe in SUSP]
     lines.append("")

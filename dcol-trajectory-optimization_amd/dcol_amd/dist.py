@@ -45,6 +45,93 @@ def shard_sizes(B: int, world: int, balanced: bool) -> list[int]:
     return [int(bounds[r + 1] - bounds[r]) for r in range(world)]
 
 
+# ---------------------------------------------------------------------------------------
+# When does sharding pay?  (BASELINE north star: "the pair batch shards across GPUs ... when
+# the batch is large enough")
+#
+# A sharded step = the rank's own solve of B / N pairs + ONE all-gather of every rank's
+# records (REC doubles per pair) so that each rank holds the whole batch.  The solve time of
+# b pairs on one MI355X is measured (bench.py mixed1m.shards: rank 0's class-balanced shard of
+# the configs[4] batch solved alone, the plan policy of the library -- packed launches for
+# mid-size plans); the all-gather is MODELLED, because this pool has no multi-GPU node to
+# time RCCL on: each rank receives (N - 1) / N of the gathered bytes, at a bus bandwidth of
+# GATHER_BUS_GBPS (RCCL's all-gather bus bandwidth on an 8-GPU xGMI node is of the order of
+# 300 GB/s for messages of this size -- a stated assumption, not a measurement here) plus a
+# fixed GATHER_LAT_MS per collective; GATHER_IDEAL_GBPS is the 7 xGMI links x ~153 GB/s
+# ingress bound of one MI355X.
+GATHER_BUS_GBPS = 300.0
+GATHER_IDEAL_GBPS = 7 * 153.0
+GATHER_LAT_MS = 0.03
+
+# one-GPU solve time of b configs[4] pairs (ms): rank 0's class-balanced shard of the 1M
+# mixed batch at world 1M / b, solved alone on one MI355X with the round-6 plan policy (packed
+# launches for mid-size plans, fused ones for small plans), K steps back to back on one stream
+# (tools/shard_bench.py, profiles/r06_d/sweep.log)
+SOLVE_CURVE_MS = ((245, 0.043), (1_954, 0.045), (7_813, 0.048), (15_625, 0.081), (31_250, 0.093),
+                  (62_500, 0.099), (125_000, 0.1435), (250_000, 0.268), (500_000, 0.507), (1_000_000, 0.874))
+
+
+def gather_ms(B: int, world: int, bus_gbps: float = GATHER_BUS_GBPS, lat_ms: float = GATHER_LAT_MS) -> float:
+    """Modelled time of the step's all-gather of B records over `world` ranks (ms)."""
+    if world <= 1:
+        return 0.0
+    cap = -(-int(B) // world)
+    total = world * cap * REC * 8.0
+    return lat_ms + total * (world - 1) / world / (bus_gbps * 1e9) * 1e3
+
+
+def solve_ms(b: float, curve=SOLVE_CURVE_MS) -> float:
+    """One-GPU solve time of b pairs (ms): log-log interpolation of the measured curve,
+    linear extrapolation past its ends (the time per pair of the last / first segment)."""
+    pts = sorted(curve)
+    xs = np.log([p[0] for p in pts])
+    ys = np.log([p[1] for p in pts])
+    x = np.log(max(float(b), 1.0))
+    if x <= xs[0]:
+        return float(np.exp(ys[0]))            # below the curve: a latency floor
+    if x >= xs[-1]:
+        return float(pts[-1][1] * b / pts[-1][0])   # beyond it: throughput-bound
+    return float(np.exp(np.interp(x, xs, ys)))
+
+
+def sharded_step_ms(B: int, world: int, curve=SOLVE_CURVE_MS, bus_gbps: float = GATHER_BUS_GBPS) -> float:
+    """Projected step of B pairs over `world` GPUs: the largest shard's solve + the all-gather."""
+    return solve_ms(-(-int(B) // max(world, 1)), curve) + gather_ms(B, world, bus_gbps)
+
+
+def shard_crossover(world: int, curve=SOLVE_CURVE_MS, bus_gbps: float = GATHER_BUS_GBPS,
+                    lo: int = 1_000, hi: int = 1 << 27) -> int | None:
+    """B*: the smallest batch for which `world` GPUs (shards + one all-gather) beat one GPU
+    on the same batch, from the solve curve and the gather model; None if they never do
+    below `hi`.  Bisection on a log grid (the difference is monotone past the latency
+    floor for these curves)."""
+    if world <= 1:
+        return None
+
+    def gain(b):
+        return solve_ms(b, curve) - sharded_step_ms(b, world, curve, bus_gbps)
+    grid = np.unique(np.geomspace(lo, hi, 200).astype(np.int64))
+    ok = [int(b) for b in grid if gain(b) > 0]
+    if not ok:
+        return None
+    b0 = ok[0]
+    i = int(np.searchsorted(grid, b0))
+    a = int(grid[i - 1]) if i > 0 else lo
+    while b0 - a > max(1, a // 1000):        # refine between the last loss and the first gain
+        m = (a + b0) // 2
+        if gain(m) > 0:
+            b0 = m
+        else:
+            a = m
+    return b0
+
+
+def should_shard(B: int, world: int, curve=SOLVE_CURVE_MS, bus_gbps: float = GATHER_BUS_GBPS) -> bool:
+    """True if sharding B pairs over `world` GPUs (one all-gather) is projected to beat
+    solving them on one GPU -- the caller's decision before dcol_prox_batch_multi_gpu."""
+    return world > 1 and sharded_step_ms(B, world, curve, bus_gbps) < solve_ms(B, curve)
+
+
 def _ints(rec):
     """[n, REC] float64 records -> [n, 2] int32 (status, iters) of the last slot"""
     return np.ascontiguousarray(rec[:, 13]).view(np.int32).reshape(-1, 2)

@@ -441,16 +441,25 @@ def test_pair_server_gives_way_to_batch_plans(engine, monkeypatch):
     assert engine.pair_server_running()
     engine.solve_pair(ball, box, grad="envelope")     # mismatching flags: launched, server stays
     assert engine.pair_server_running()
-    # a small plan (latency-bound: cannot fill the GPU) leaves the server resident, so a caller
-    # interleaving small batches with drop-in calls does not restart it at every pair call
+    # a small plan (latency-bound: cannot fill the GPU) on a stream of its own leaves the
+    # server resident, so a caller interleaving small batches with drop-in calls does not
+    # restart it at every pair call (made, with its buffers, while no server is resident:
+    # synchronous HIP calls wait for the server's blocking stream; a null-stream launch makes
+    # it leave, dcol_capi.cpp plan_run_rec)
+    engine.stop_pair_server()
     small = engine.plan(ids[s1[:200]], ids[s2[:200]], cache=False)
     sd1, sd2 = d1[:, :200].contiguous(), d2[:, :200].contiguous()
+    sout = alloc_outputs(200, dev, want_grad=True, want_contact=False)
+    side = torch.cuda.Stream(dev)
+    assert small.launch_form == "buckets" and small.num_launches == 1
+    np.testing.assert_array_equal(_bits([engine.solve_pair(ball, box, grad=None)]), _bits([ref_pair]))
     starts0 = engine.pair_stats()["server_starts"]
-    for _ in range(20):
-        small.run(sd1, sd2, grad="fd", contact=False, stream=stream)
-        stream.synchronize()
+    for i in range(20):
+        small.run(sd1, sd2, grad="fd", contact=False, out=sout, stream=side)
+        side.synchronize()
+        assert engine.pair_server_running(), i
         np.testing.assert_array_equal(_bits([engine.solve_pair(ball, box, grad=None)]), _bits([ref_pair]))
-    assert engine.pair_stats()["server_starts"] == starts0
+        assert engine.pair_stats()["server_starts"] == starts0, (i, engine.pair_stats())
     assert engine.pair_server_running()
     engine.stop_pair_server()
     stopped, resident = min(t["stopped"]), min(t["resident"])

@@ -134,7 +134,7 @@ def test_packed_launch_bitwise_equal_to_bucket_launches(engine, world):
     solver copies as the per-bucket kernels: rank 0's class-balanced shard of the configs[4]
     batch at world 8 (125k pairs) and 32 (31k: a small plan the fused kernel cannot take,
     packed instead of fanned out) gives BITWISE the outputs of the same buckets launched one
-    by one (fuse=False), and of the shard's pairs inside the whole 1M plan."""
+    by one (fuse=False, world 8), and of the shard's pairs inside the whole 1M plan."""
     import torch
     import bench
     from dcol_amd import alloc_outputs
@@ -149,20 +149,22 @@ def test_packed_launch_bitwise_equal_to_bucket_launches(engine, world):
     d2 = torch.from_numpy(np.ascontiguousarray(p2[mine].T)).to(dev)
     packed = engine.plan(ids[s1[mine]], ids[s2[mine]], cache=False)
     assert packed.launch_form == "packed" and packed.num_launches == 1
-    apart = engine.plan(ids[s1[mine]], ids[s2[mine]], cache=False, fuse=False)
-    assert apart.launch_form == "buckets"
     a = packed.run(d1, d2, grad="fd", contact=True)
-    b = apart.run(d1, d2, grad="fd", contact=True)
-    torch.cuda.synchronize()
-    for k in ("status", "iters", "alpha", "grad", "contact"):
-        assert torch.equal(a[k], b[k]), k
-    if world == 8:   # against the whole batch's plan (one launch per bucket, throughput configurations)
-        whole = engine.plan(ids[s1], ids[s2], cache=False)
-        w1 = torch.from_numpy(np.ascontiguousarray(p1.T)).to(dev)
-        w2 = torch.from_numpy(np.ascontiguousarray(p2.T)).to(dev)
-        out = alloc_outputs(B, dev, want_grad=True, want_contact=False)
-        whole.run(w1, w2, grad="fd", contact=False, out=out)
-        sel = torch.from_numpy(mine).to(dev)
-        for k in ("status", "iters", "alpha"):
-            assert torch.equal(out[k][sel], a[k]), k
-        assert torch.equal(out["grad"][:, sel], a["grad"])
+    if world == 8:   # a mid-size plan: the same buckets launched one by one
+        apart = engine.plan(ids[s1[mine]], ids[s2[mine]], cache=False, fuse=False)
+        assert apart.launch_form == "buckets"
+        b = apart.run(d1, d2, grad="fd", contact=True)
+        torch.cuda.synchronize()
+        for k in ("status", "iters", "alpha", "grad", "contact"):
+            assert torch.equal(a[k], b[k]), k
+    # against the whole batch's plan (one launch per bucket, throughput configurations; a
+    # small plan unfused would have taken latency configurations instead)
+    whole = engine.plan(ids[s1], ids[s2], cache=False)
+    w1 = torch.from_numpy(np.ascontiguousarray(p1.T)).to(dev)
+    w2 = torch.from_numpy(np.ascontiguousarray(p2.T)).to(dev)
+    out = alloc_outputs(B, dev, want_grad=True, want_contact=False)
+    whole.run(w1, w2, grad="fd", contact=False, out=out)
+    sel = torch.from_numpy(mine).to(dev)
+    for k in ("status", "iters", "alpha"):
+        assert torch.equal(out[k][sel], a[k]), k
+    assert torch.equal(out["grad"][:, sel], a["grad"])

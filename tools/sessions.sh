@@ -70,5 +70,16 @@ case $P in
     OUT=$O $S \
       "sweep|700|python3 tools/shard_bench.py --sweep --worlds $W --only=default,pack_off,small_fanout" \
       "tests|1000|python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread" ;;
+  tests)      # the GPU suite (or the tests named by $K, a pytest -k expression)
+    OUT=$O $S "tests|1000|python3 -u -m pytest tests -m gpu -q -s --timeout 300 --timeout-method thread ${K:+-k \"$K\"}" ;;
+  quick)      # tests named by $K, then a short bench line (every section but the CPU baselines)
+    OUT=$O $S "tests|900|python3 -u -m pytest tests -m gpu -q -s --timeout 300 --timeout-method thread -k \"$K\"" \
+      "bench|400|python3 bench.py --no-cpu --steps 100 --warmup 20" ;;
+  shards5)    # the two-family packed launch by threshold; tests named by $K
+    W=1,2,3,4,6,8,16,32,64,128,512,4096
+    OUT=$O $S \
+      "sweep|700|python3 tools/shard_bench.py --sweep --worlds $W --only=default,pack_all,pack_off" \
+      "trace125k|200|rocprofv3 --kernel-trace -f csv -d $O/trace125k -o run -- python3 tools/shard_bench.py --worlds 8 --steps 20" \
+      "tests|900|python3 -u -m pytest tests -m gpu -q -s --timeout 300 --timeout-method thread -k \"$K\"" ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
