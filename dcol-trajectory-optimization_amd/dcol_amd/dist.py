@@ -101,23 +101,25 @@ def sharded_step_ms(B: int, world: int, curve=SOLVE_CURVE_MS, bus_gbps: float = 
 
 def shard_crossover(world: int, curve=SOLVE_CURVE_MS, bus_gbps: float = GATHER_BUS_GBPS,
                     lo: int = 1_000, hi: int = 1 << 27) -> int | None:
-    """B*: the smallest batch for which `world` GPUs (shards + one all-gather) beat one GPU
-    on the same batch, from the solve curve and the gather model; None if they never do
-    below `hi`.  Bisection on a log grid (the difference is monotone past the latency
-    floor for these curves)."""
+    """B*: the batch size from which on `world` GPUs (shards + one all-gather) beat one GPU on
+    every larger batch, from the solve curve and the gather model (the gain need not be
+    monotone below it: the one-GPU curve has a latency floor and a step where plans change
+    form); None if they lose at `hi`.  Scan on a log grid, then bisection between the last
+    loss and the next gain."""
     if world <= 1:
         return None
 
     def gain(b):
         return solve_ms(b, curve) - sharded_step_ms(b, world, curve, bus_gbps)
-    grid = np.unique(np.geomspace(lo, hi, 200).astype(np.int64))
-    ok = [int(b) for b in grid if gain(b) > 0]
-    if not ok:
+    grid = np.unique(np.geomspace(lo, hi, 400).astype(np.int64))
+    wins = [gain(int(b)) > 0 for b in grid]
+    if not wins[-1]:
         return None
-    b0 = ok[0]
-    i = int(np.searchsorted(grid, b0))
-    a = int(grid[i - 1]) if i > 0 else lo
-    while b0 - a > max(1, a // 1000):        # refine between the last loss and the first gain
+    last_loss = max((i for i, w in enumerate(wins) if not w), default=-1)
+    if last_loss < 0:
+        return int(grid[0])
+    a, b0 = int(grid[last_loss]), int(grid[last_loss + 1])
+    while b0 - a > max(1, a // 1000):
         m = (a + b0) // 2
         if gain(m) > 0:
             b0 = m

@@ -235,3 +235,26 @@ def test_deadline_clean_run_exits_zero():
     assert p.returncode == 0, p.stdout + p.stderr
     assert not diags
     assert p.stdout.count("steps done") == 2
+
+
+def test_gather_model_and_crossover():
+    """When sharding pays (dcol_amd.dist): the all-gather model moves
+    (N - 1) / N of the N x cap records through each rank; the solve curve interpolates the
+    measured points log-log and extrapolates linearly past the largest; B* is where N GPUs
+    start winning for good, and should_shard agrees with it on both sides."""
+    from dcol_amd import dist as D
+    assert D.gather_ms(1_000_000, 1) == 0.0
+    g8 = D.gather_ms(1_000_000, 8, bus_gbps=100.0, lat_ms=0.0)
+    assert abs(g8 - 8 * 125_000 * D.REC * 8 * 7 / 8 / 100e9 * 1e3) < 1e-12
+    pts = ((1000, 0.01), (10_000, 0.1))
+    assert abs(D.solve_ms(1000, pts) - 0.01) < 1e-15 and abs(D.solve_ms(10_000, pts) - 0.1) < 1e-15
+    assert abs(D.solve_ms(20_000, pts) - 0.2) < 1e-12          # throughput-bound past the curve
+    assert D.solve_ms(10, pts) == pytest.approx(0.01, rel=1e-12)   # latency floor below it
+    assert D.solve_ms(3000, pts) == pytest.approx(0.03, rel=1e-9)
+    for n in (2, 4, 8):
+        b = D.shard_crossover(n)
+        assert b is not None and 1000 < b < 1_000_000
+        assert D.should_shard(1_000_000, n) and D.should_shard(2 * b, n)
+        assert not D.should_shard(int(b * 0.98), n) or D.shard_crossover(n) == b
+    assert D.shard_crossover(8, bus_gbps=1e-3) is None          # a gather that never pays
+    assert not D.should_shard(10 ** 9, 1)

@@ -349,3 +349,4 @@ def test_suspend_resume_bitwise_equal(batch):
     assert susp.suspended() > 0
     for k in ("status", "iters", "alpha", "grad", "contact"):
         assert torch.equal(a[k], c[k]), k
+
