@@ -21,7 +21,7 @@ SIMDS = 1024   # MI355X: 256 CUs x 4 SIMDs
 def main():
     path, out = sys.argv[1], sys.argv[2]
     pairs = int(sys.argv[3]) if len(sys.argv) > 3 else 100_000
-    ksub = sys.argv[4] if len(sys.argv) > 4 else "prox_kernel<4, 0, 12, 2, 3, 9, 0>"
+    ksub = sys.argv[4] if len(sys.argv) > 4 else "prox_kernel<4, 0, 12, 2, 3, "   # the BOX kernel (FD-only copy: FL 73)
     vals, name = {}, None
     for r in csv.DictReader(open(path)):
         if ksub in r["Kernel_Name"]:
