@@ -1091,7 +1091,9 @@ int plan_run_rec(const dcol_plan* p, const double* pose1, const double* pose2, d
             e = hipMemsetAsync(L.d_susp_count, 0, sizeof(int32_t), ls);
             if (e == hipSuccess) e = launch_susp(L.N, L.nsoc, L.omax, L.lpp, L.flags(), L.oe, b, ls);
         } else {
-            e = launch_variant(L.N, L.nsoc, L.omax, L.lpp, L.flags() | fdonly, a, ls, L.oe);
+            const int split = (L.oe > 0 && L.lpp == 2 && split_enabled() && split_built(L.N, L.nsoc, L.omax, L.oe))
+                                  ? LF_SPLIT : 0;
+            e = launch_variant(L.N, L.nsoc, L.omax, L.lpp, L.flags() | fdonly | split, a, ls, L.oe);
         }
         if (e != hipSuccess) break;
     }

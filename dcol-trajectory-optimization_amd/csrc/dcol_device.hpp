@@ -333,11 +333,13 @@ DCOL_HD void dcm_jacobian(const double p[3], double dQ[3][9]) {
 template <int D>
 DCOL_HD double tail_dot(const double* v, const double* w) {
     if constexpr (D == 4) return v[1] * w[1] + v[2] * w[2] + v[3] * w[3];
+    else if constexpr (D == 2) return v[1] * w[1];   // (a SPLIT lane's half: the caller completes the sum)
     else return v[1] * w[1] + v[2] * w[2];
 }
 template <int D>
 DCOL_HD double full_dot(const double* v, const double* w) {
     if constexpr (D == 4) return v[0] * w[0] + v[1] * w[1] + v[2] * w[2] + v[3] * w[3];
+    else if constexpr (D == 2) return v[0] * w[0] + v[1] * w[1];
     else return v[0] * w[0] + v[1] * w[1] + v[2] * w[2];
 }
 
@@ -498,6 +500,8 @@ __device__ __forceinline__ void dpp_check() {
     unsigned src;
     if (CTRL == 0xB1) src = lane ^ 1u;
     else if (CTRL == 0x4E) src = lane ^ 2u;
+    else if (CTRL == 0xA0) src = lane & ~1u;
+    else if (CTRL == 0xF5) src = lane | 1u;
     else if (CTRL == 0x141) src = (lane & ~7u) | (7u - (lane & 7u));
     else src = (lane & ~15u) | (15u - (lane & 15u));
     const unsigned long long exec = __builtin_amdgcn_read_exec();
@@ -524,11 +528,15 @@ __device__ __forceinline__ double dpp_d(double v) {
 #define DCOL_XOR2(v) dpp_d<0x4E>(v)   // quad_perm [2,3,0,1]
 #define DCOL_HMIR(v) dpp_d<0x141>(v)  // row_half_mirror: lane i <-> 7-i within 8 lanes
 #define DCOL_RMIR(v) dpp_d<0x140>(v)  // row_mirror: lane i <-> 15-i within 16 lanes
+#define DCOL_BC0(v) dpp_d<0xA0>(v)    // quad_perm [0,0,2,2]: a lane pair's first lane to both
+#define DCOL_BC1(v) dpp_d<0xF5>(v)    // quad_perm [1,1,3,3]: its second lane to both
 #else
 #define DCOL_XOR1(v) (__builtin_trap(), (v))   // multi-lane groups run on the GPU only
 #define DCOL_XOR2(v) (__builtin_trap(), (v))
 #define DCOL_HMIR(v) (__builtin_trap(), (v))
 #define DCOL_RMIR(v) (__builtin_trap(), (v))
+#define DCOL_BC0(v) (__builtin_trap(), (v))
+#define DCOL_BC1(v) (__builtin_trap(), (v))
 #endif
 
 template <int LPP>
@@ -639,9 +647,20 @@ struct Grp<4> {
 // 4 or 3 instead of 6, and it holds 4 or 3 doubles of G instead of 6.  The rows' reference
 // order within a pair changes, i.e. the lane sums add the same terms in another order
 // (rounding level); parity is pinned by iteration-count equality on every golden vector.
+// SPLIT (round 6): the one ball SOC block of an NSOC = 1 pair at LPP 2
+// split over the pair's two lanes -- lane q holds the block's coordinates 2q, 2q + 1 (its s,
+// z, r and every per-coordinate product), instead of the whole block in lane 0 while lane 1
+// idles through the SOC work.  The block's scalars (J(s), J(z), w'v, the line-search sums)
+// are partial sums over a lane's coordinates completed by one DPP exchange (R::sum); the
+// head coordinate's value reaches lane 1 by one more (bc0); the NT point w is held whole in
+// both lanes.  The structured ball rows (R, X) are replicated; the block's share of the
+// normal matrix and of G'G in initialize() is taken in lane 0 (lane 1 adds zeros), G_b'v per
+// coordinate in its own lane (the group sum adds them).  Rounding-level against the one-lane
+// block (sums in another order); pinned by iteration-count equality against the C oracle.
 template <int N, int NSOC, int OMAX, int LPP, bool BALL = false, bool CONE = false, int OE = 0, bool GLDS = false,
-          bool BOX = false>
+          bool BOX = false, bool SPLIT = false>
 struct Solver {
+    static_assert(!SPLIT || (BALL && NSOC == 1 && LPP == 2 && !GLDS && !BOX), "SPLIT: one ball block over two lanes");
     static_assert(OMAX % LPP == 0, "OMAX must be a multiple of LPP");
     static_assert(!(BALL && CONE) && (!CONE || N == 4), "CONE: cone-only SOC blocks of N = 4 pairs");
     static_assert(OE % LPP == 0 && OE <= OMAX && (OE == 0 || (N == 5 || N == 6)), "PART: N = 5 / 6, OE % LPP == 0");
@@ -660,7 +679,8 @@ struct Solver {
     static constexpr int EL = OE / LPP;                // PART: extra-column slots per lane (the last EL)
     static constexpr int PL = OR - EL;                 // PART: pose slots per lane (the first PL)
     static constexpr int SS = (NSOC + LPP - 1) / LPP;  // SOC slots per lane
-    static constexpr int SD = CONE ? 3 : 4;            // rows per SOC slot (cones unpadded in CONE)
+    static constexpr int SD = CONE ? 3 : (SPLIT ? 2 : 4);   // rows per SOC slot (cones unpadded in CONE;
+                                                            // SPLIT: this lane's half of the block)
     static constexpr int M = OR + SD * SS;             // lane-local rows
     static constexpr int SSA = SS > 0 ? SS : 1;
     static constexpr int MG = (BALL || CONE) ? OR : M; // rows held densely in G
@@ -872,7 +892,7 @@ struct Solver {
         const int own0 = S1.soc_kind != SOC_NONE ? 0 : 1;
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
-            const int gb = b * LPP + q;
+            const int gb = SPLIT ? 0 : b * LPP + q;   // SPLIT: both lanes hold (half of) block 0
             vs[b] = gb < NSOC;
             const bool p2 = (gb == 0) ? (own0 == 1) : true;
             soc_owner[b] = p2 ? 1 : 0;
@@ -888,13 +908,17 @@ struct Solver {
                 const int off = xoff(p2);
                 sv[b] = one;
                 sR[b] = vs[b] ? (p2 ? S2.R : S1.R) : 0.0;
-                r[OR + SD * b] = 0.0;
+                if constexpr (!SPLIT) r[OR + SD * b] = 0.0;
 #pragma unroll
                 for (int k = 0; k < 3; ++k) {
                     const double c0 = (nx >= 1) ? Qe[3 * k] : 0.0, c1 = (nx >= 2) ? Qe[3 * k + 1] : 0.0;
 #pragma unroll
                     for (int j = 4; j < N; ++j) sX[b][k][j - 4] = one * excol(j, off, c0, c1);
-                    r[OR + SD * b + 1 + k] = vs[b] ? -re[k] : 0.0;
+                    if constexpr (!SPLIT) r[OR + SD * b + 1 + k] = vs[b] ? -re[k] : 0.0;
+                }
+                if constexpr (SPLIT) {   // h of this lane's coordinates: 0 for the head, -re[c - 1]
+                    r[OR] = q ? -re[1] : 0.0;
+                    r[OR + 1] = q ? -re[2] : -re[0];
                 }
             } else if constexpr (CONE) {
                 // cone block, problem_matrices.py:138-145: rows -E Qe' (E = diag(tanb, 1, 1)),
@@ -973,6 +997,144 @@ struct Solver {
         }
     }
 
+    // -------- SOC block arithmetic (NT_scaling.py:340-463, pdip.py:25-200): the SD-row
+    // templates, or under SPLIT this lane's two coordinates c = 2q, 2q + 1 of the one block --
+    // lane 0's value of x in both lanes (the head coordinate: lane 0's local slot 0)
+    DCOL_HD double bc0(double x) const {
+        if constexpr (LPP == 2) return DCOL_BC0(x);
+        return x;
+    }
+    // sums over the block of v_c w_c: the tail (c >= 1) / every coordinate
+    DCOL_HD double sp_tail(const double* v, const double* w) const {
+        return R::sum(q ? fma(v[0], w[0], v[1] * w[1]) : v[1] * w[1]);
+    }
+    DCOL_HD double sp_full(const double* v, const double* w) const { return R::sum(fma(v[0], w[0], v[1] * w[1])); }
+    // w1 at this lane's local slot e (W whole in both lanes; slot 0 of lane 0 is the head)
+    DCOL_HD double wloc(const SocNT& W, int e) const {
+        return e == 0 ? (q ? W.w1[1] : W.w0) : (q ? W.w1[2] : W.w1[0]);
+    }
+    DCOL_HD double wtail(const SocNT& W, const double* v) const {   // w1'v1 over the block
+        return R::sum(q ? fma(W.w1[1], v[0], W.w1[2] * v[1]) : W.w1[0] * v[1]);
+    }
+    DCOL_HD void nt(const double* sl, const double* zl, SocNT& W) const {
+        if constexpr (!SPLIT) {
+            soc_nt<SD>(sl, zl, W);
+        } else {
+            const double z0 = bc0(zl[0]), s0 = bc0(sl[0]);
+            const double Jz = z0 * z0 - sp_tail(zl, zl);
+            const double Js = s0 * s0 - sp_tail(sl, sl);
+            const double iz = frsqrt(Jz);
+            const double is = frsqrt(Js);
+            double zb[2], sb[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                zb[k] = zl[k] * iz;
+                sb[k] = sl[k] * is;
+            }
+            const double dot = sp_full(zb, sb);
+            const double i2g = 0.5 * frsqrt((1.0 + dot) * 0.5);   // 1/(2 gamma)
+            const double wl0 = (q ? sb[0] - zb[0] : sb[0] + zb[0]) * i2g, wl1 = (sb[1] - zb[1]) * i2g;
+            W.w0 = DCOL_BC0(wl0);   // w whole in both lanes: coordinates 0, 1 from lane 0, 2, 3 from lane 1
+            W.w1[0] = DCOL_BC0(wl1);
+            W.w1[1] = DCOL_BC1(wl0);
+            W.w1[2] = DCOL_BC1(wl1);
+            W.bf = frcp1(W.w0 + 1.0);
+#if defined(__HIP_DEVICE_COMPILE__)
+            W.lis[0] = (Js >= 1e-25) ? is : 3162277660168.3794;
+            W.lis[1] = (Jz >= 1e-25) ? iz : 3162277660168.3794;
+            const double u = (Js * is) * iz;
+            const double ie = frsqrt(u);
+            W.eta = (Jz != 0.0) ? u * ie : 1.0;                     // quirk Q9
+            W.ieta = (Jz != 0.0) ? ie : 1.0;
+#else
+            W.lis[0] = frsqrt(fmax(Js, 1e-25));
+            W.lis[1] = frsqrt(fmax(Jz, 1e-25));
+            W.eta = (Jz != 0.0) ? sqrt(sqrt(Js * frcp1(Jz))) : 1.0;
+            W.ieta = frcp1(W.eta);
+#endif
+            W.lrc[0] = frcp1(fma(s0, W.lis[0], 1.0));
+            W.lrc[1] = frcp1(fma(z0, W.lis[1], 1.0));
+        }
+    }
+    DCOL_HD void wmul(const SocNT& W, const double* v, double* out) const {   // W v
+        if constexpr (!SPLIT) {
+            soc_mul<SD>(W, v, out);
+        } else {
+            const double d = wtail(W, v), v0 = bc0(v[0]);
+            const double c = W.bf * d;
+            const double w = wloc(W, 0), w1 = wloc(W, 1);
+            out[0] = q ? W.eta * (v0 * w + v[0] + c * w) : W.eta * (W.w0 * v0 + d);
+            out[1] = W.eta * (v0 * w1 + v[1] + c * w1);
+        }
+    }
+    DCOL_HD void wsolve(const SocNT& W, const double* v, double* out) const {   // W^-1 v
+        if constexpr (!SPLIT) {
+            soc_solve<SD>(W, v, out);
+        } else {
+            const double d = wtail(W, v), v0 = bc0(v[0]);
+            const double c = W.bf * d;
+            const double w = wloc(W, 0), w1 = wloc(W, 1);
+            out[0] = q ? W.ieta * (v[0] - v0 * w + c * w) : W.ieta * (W.w0 * v0 - d);
+            out[1] = W.ieta * (v[1] - v0 * w1 + c * w1);
+        }
+    }
+    DCOL_HD void w2inv(const SocNT& W, const double* v, double* out) const {   // W^-2 v
+        if constexpr (!SPLIT) {
+            soc_w2inv<SD>(W, v, out);
+        } else {
+            const double d = wtail(W, v), v0 = bc0(v[0]);
+            const double e2 = W.ieta * W.ieta;
+            const double tw = 2.0 * W.w0;
+            const double c = 2.0 * d - tw * v0;
+            out[0] = q ? e2 * (v[0] + c * wloc(W, 0)) : e2 * ((tw * W.w0 - 1.0) * v0 - tw * d);
+            out[1] = e2 * (v[1] + c * wloc(W, 1));
+        }
+    }
+    DCOL_HD void cprod(const double* u, const double* v, double* out) const {   // u o v
+        if constexpr (!SPLIT) {
+            soc_prod<SD>(u, v, out);
+        } else {
+            const double sd = sp_full(u, v), u0 = bc0(u[0]), v0 = bc0(v[0]);
+            out[0] = q ? u0 * v[0] + v0 * u[0] : sd;
+            out[1] = u0 * v[1] + v0 * u[1];
+        }
+    }
+    DCOL_HD void ciprod(const double* u, const double* w, double* out) const {   // u \ w
+        if constexpr (!SPLIT) {
+            soc_iprod<SD>(u, w, out);
+        } else {
+            const double u0 = bc0(u[0]), w0 = bc0(w[0]);
+            const double rho = u0 * u0 - sp_tail(u, u);
+            const double nu = sp_tail(u, w);
+            const double irho = frcp1(rho);
+            const double iu0 = frcp1(u0);
+            const double c1 = nu * iu0 - w0;
+            const double c2 = rho * iu0;
+            out[0] = q ? irho * (c1 * u[0] + c2 * w[0]) : irho * (u0 * w0 - nu);
+            out[1] = irho * (c1 * u[1] + c2 * w[1]);
+        }
+    }
+    DCOL_HD double lsinv(const double* y, const double* d, double isn, double rc) const {   // soc_ls_inv
+        if constexpr (!SPLIT) {
+            return soc_ls_inv<SD>(y, d, isn, rc);
+        } else {
+            const double y0 = bc0(y[0]), d0 = bc0(d[0]);
+            const double zeta = y0 * d0 - sp_tail(y, d);
+            const double inu = isn * isn;
+            const double rho0 = zeta * inu;
+            const double coef = (zeta * isn + d0) * rc;
+            const double r0 = d[0] * isn - coef * (y[0] * inu);
+            const double r1 = d[1] * isn - coef * (y[1] * inu);
+            const double n2 = R::sum(q ? fma(r0, r0, r1 * r1) : r1 * r1);
+#if defined(__HIP_DEVICE_COMPILE__)
+            const double n1 = n2 > 0.0 ? n2 * frsqrt(n2) : 0.0;
+#else
+            const double n1 = sqrt(n2);
+#endif
+            return fmax(1.0, n1 - rho0);
+        }
+    }
+
     // -------- small dense helpers ------------------------------------------------------
     DCOL_HD double rowdot(int k, const double* v) const {
         if constexpr (BOX)
@@ -999,6 +1161,20 @@ struct Solver {
     }
     // BALL: row e of SOC slot b times v
     DCOL_HD double ball_row(int k, const double* v) const {
+        if constexpr (SPLIT) {   // this lane's coordinate c = 2q + e: c = 0 the head row, else [-e_(c-1) | 0 | X_(c-1)]
+            const int e = k - OR;
+            if (e == 0) {
+                const double a = q ? v[1] : v[3];
+                double acc = fma(q ? -sv[0] : -sR[0], a, 0.0);
+#pragma unroll
+                for (int i = 0; i < NX; ++i) acc = fma(q ? sX[0][1][i] : 0.0, v[4 + i], acc);
+                return acc;
+            }
+            double acc = -sv[0] * (q ? v[2] : v[0]);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) acc = fma(q ? sX[0][2][i] : sX[0][0][i], v[4 + i], acc);
+            return acc;
+        }
         const int b = (k - OR) / 4, e = (k - OR) % 4;
         // an fma (as the dense row's last term), not a bare product the optimiser could
         // contract into a consumer differently in different kernels (fused == split bitwise)
@@ -1026,6 +1202,17 @@ struct Solver {
 #pragma unroll
                 for (int j = 0; j < 3; ++j) out[j] += cqx(b, e, j) * v[e];
                 if (e == 0) out[3] += ccx(b) * v[0];
+            }
+        } else if constexpr (SPLIT) {   // this lane's coordinates (c = 2q, 2q + 1); the group sum adds the other's
+            const double t0 = v[0], t1 = v[1];
+            out[0] = fma(q ? 0.0 : -sv[0], t1, out[0]);
+            out[1] = fma(q ? -sv[0] : 0.0, t0, out[1]);
+            out[2] = fma(q ? -sv[0] : 0.0, t1, out[2]);
+            out[3] = fma(q ? 0.0 : -sR[0], t0, out[3]);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                out[4 + i] = fma(q ? sX[0][1][i] : 0.0, t0, out[4 + i]);
+                out[4 + i] = fma(q ? sX[0][2][i] : sX[0][0][i], t1, out[4 + i]);
             }
         } else if constexpr (BALL) {
 #pragma unroll
@@ -1112,7 +1299,9 @@ struct Solver {
                     mm[l][k] = mm[k][l];
                 }
             }
-            const double v = sv[b], R = sR[b];
+            // (SPLIT: the whole block's share in lane 0, zeros from lane 1 -- W is whole in both)
+            const double own = (!SPLIT || q == 0) ? 1.0 : 0.0;
+            const double v = sv[b] * own, R = sR[b] * own;
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
 #pragma unroll
@@ -1121,13 +1310,17 @@ struct Solver {
             }
             Hm[3][3] = fma(R * R, m00, Hm[3][3]);
             if constexpr (NX > 0) {
-                double mx[3][NXA], m0x[NXA];
+                double mx[3][NXA], m0x[NXA], X[3][NXA];
+#pragma unroll
+                for (int k = 0; k < 3; ++k)
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) X[k][i] = SPLIT ? sX[b][k][i] * own : sX[b][k][i];
 #pragma unroll
                 for (int i = 0; i < NX; ++i) {
-                    m0x[i] = m0[0] * sX[b][0][i] + m0[1] * sX[b][1][i] + m0[2] * sX[b][2][i];
+                    m0x[i] = m0[0] * X[0][i] + m0[1] * X[1][i] + m0[2] * X[2][i];
 #pragma unroll
                     for (int k = 0; k < 3; ++k)
-                        mx[k][i] = mm[k][0] * sX[b][0][i] + mm[k][1] * sX[b][1][i] + mm[k][2] * sX[b][2][i];
+                        mx[k][i] = mm[k][0] * X[0][i] + mm[k][1] * X[1][i] + mm[k][2] * X[2][i];
                 }
 #pragma unroll
                 for (int i = 0; i < NX; ++i) {
@@ -1136,7 +1329,7 @@ struct Solver {
                     Hm[3][4 + i] = fma(-R, m0x[i], Hm[3][4 + i]);
 #pragma unroll
                     for (int i2 = i; i2 < NX; ++i2)
-                        Hm[4 + i][4 + i2] += sX[b][0][i] * mx[0][i2] + sX[b][1][i] * mx[1][i2] + sX[b][2][i] * mx[2][i2];
+                        Hm[4 + i][4 + i2] += X[0][i] * mx[0][i2] + X[1][i] * mx[1][i2] + X[2][i] * mx[2][i2];
                 }
             }
         } else {
@@ -1252,7 +1445,8 @@ struct Solver {
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
             const double* p = v + OR + SD * b;
-            const double res = p[0] - sqrt(tail_dot<SD>(p, p));
+            const double res = SPLIT ? bc0(p[0]) - sqrt(R::sum(q ? fma(p[0], p[0], p[1] * p[1]) : p[1] * p[1]))
+                                     : p[0] - sqrt(tail_dot<SD>(p, p));
             socv = (vs[b] & (res <= 0.0)) ? fmax(socv, -res) : socv;
         }
         any = R::max(any);
@@ -1266,7 +1460,8 @@ struct Solver {
 #pragma unroll
             for (int k = 0; k < OR; ++k) v[k] = live<FULL>(k) ? v[k] + sh : v[k];
 #pragma unroll
-            for (int b = 0; b < SS; ++b) v[OR + SD * b] = vs[b] ? v[OR + SD * b] + sh : v[OR + SD * b];
+            for (int b = 0; b < SS; ++b)   // (the head coordinate: lane 0's under SPLIT)
+                v[OR + SD * b] = (vs[b] && (!SPLIT || q == 0)) ? v[OR + SD * b] + sh : v[OR + SD * b];
         }
     }
 
@@ -1318,19 +1513,23 @@ struct Solver {
             for (int b = 0; b < SS; ++b) {
                 const int k0 = OR + SD * b;
                 soc_gtv(b, r + k0, gth);
-                H[3][3] = fma(sR[b], sR[b], H[3][3]);
+                // (SPLIT: G_b'G_b from lane 0 only; G_b'h per coordinate above)
+                const double own = (!SPLIT || q == 0) ? 1.0 : 0.0;
+                const double sRb = sR[b] * own, svb = sv[b] * own;
+                H[3][3] = fma(sRb, sRb, H[3][3]);
 #pragma unroll
                 for (int j = 0; j < 3; ++j) {
-                    H[j][j] = fma(sv[b], sv[b], H[j][j]);
+                    H[j][j] = fma(svb, svb, H[j][j]);
 #pragma unroll
-                    for (int i = 0; i < NX; ++i) H[j][4 + i] = fma(-sv[b], sX[b][j][i], H[j][4 + i]);
+                    for (int i = 0; i < NX; ++i) H[j][4 + i] = fma(-svb, sX[b][j][i], H[j][4 + i]);
                 }
 #pragma unroll
                 for (int i = 0; i < NX; ++i)
 #pragma unroll
                     for (int i2 = i; i2 < NX; ++i2)
 #pragma unroll
-                        for (int k = 0; k < 3; ++k) H[4 + i][4 + i2] = fma(sX[b][k][i], sX[b][k][i2], H[4 + i][4 + i2]);
+                        for (int k = 0; k < 3; ++k)
+                            H[4 + i][4 + i2] = fma(sX[b][k][i] * own, sX[b][k][i2], H[4 + i][4 + i2]);
             }
         }
         if constexpr (CONE) {                      // the cone rows, same order as dense rows
@@ -1378,7 +1577,7 @@ struct Solver {
 #pragma unroll
         for (int k = 0; k < M; ++k) {
             const bool v = k < OR ? live<FULL>(k) : vrow(k);
-            const double one = (k < OR || ((k - OR) % SD) == 0) ? 1.0 : 0.0;   // inert: e
+            const double one = (k < OR || (((k - OR) % SD) == 0 && (!SPLIT || q == 0))) ? 1.0 : 0.0;   // inert: e
             s[k] = v ? t[k] : one;
             z[k] = v ? zt[k] : one;
         }
@@ -1506,9 +1705,9 @@ struct Solver {
 #pragma unroll
             for (int b = 0; b < SS; ++b) {
                 const int k0 = OR + SD * b;
-                soc_nt<SD>(s + k0, z + k0, so[b].W);
-                soc_mul<SD>(so[b].W, z + k0, so[b].lam);
-                soc_prod<SD>(so[b].lam, so[b].lam, so[b].ll);
+                nt(s + k0, z + k0, so[b].W);
+                wmul(so[b].W, z + k0, so[b].lam);
+                cprod(so[b].lam, so[b].lam, so[b].ll);
             }
             // SOC part of the normal matrix
 #pragma unroll
@@ -1555,9 +1754,9 @@ struct Solver {
             for (int b = 0; b < SS; ++b) {
                 const int k0 = OR + SD * b;
                 double t1[SD], t2[SD];
-                soc_solve<SD>(so[b].W, dsS + SD * b, t1);
-                soc_mul<SD>(so[b].W, dzS + SD * b, t2);
-                soc_prod<SD>(t1, t2, cp + k0);
+                wsolve(so[b].W, dsS + SD * b, t1);
+                wmul(so[b].W, dzS + SD * b, t2);
+                cprod(t1, t2, cp + k0);
             }
 
             // ---- corrector (combined) direction; orthant G dx and dz are kept for the
@@ -1660,7 +1859,7 @@ struct Solver {
             double sr[SD], q[SD], bz[SD];
 #pragma unroll
             for (int e = 0; e < SD; ++e) sr[e] = s[k0 + e] + r[k0 + e];
-            soc_w2inv<SD>(so[b].W, sr, q);
+            w2inv(so[b].W, sr, q);
             if (!cp) {
                 // predictor: lambda \ ds = -lambda, so W^-1 lds = -W^-1 W z = -z exactly:
                 // W^-1 b~z = z - W^-2 (s + r) and (W^-1 b~z) - z = -W^-2 (s + r) (no soc_solve)
@@ -1673,7 +1872,7 @@ struct Solver {
             } else {
                 soc_lds(so[b], cp + k0, smu, slds[b]);
                 double m[SD];
-                soc_solve<SD>(so[b].W, slds[b], m);
+                wsolve(so[b].W, slds[b], m);
 #pragma unroll
                 for (int e = 0; e < SD; ++e) sbzt[b][e] = -q[e] - m[e];
 #pragma unroll
@@ -1703,7 +1902,7 @@ struct Solver {
         double t[SD];
 #pragma unroll
         for (int e = 0; e < SD; ++e) u[e] = rowdot(k0 + e, dx);
-        soc_w2inv<SD>(S.W, u, t);
+        w2inv(S.W, u, t);
 #pragma unroll
         for (int e = 0; e < SD; ++e) {
             dz[e] = t[e] - wbz[e];
@@ -1746,7 +1945,7 @@ struct Solver {
     DCOL_HD double orth_num(int k, const double* cp, double smu, double v) const {
         return cp ? fma(z[k], v, smu - cp[k]) : z[k] * v;
     }
-    DCOL_HD static void soc_lds(const SocState& S, const double* cp, double smu, double* out) {
+    DCOL_HD void soc_lds(const SocState& S, const double* cp, double smu, double* out) const {
         if (!cp) {                               // lambda \ (-lambda o lambda) = -lambda
 #pragma unroll
             for (int e = 0; e < SD; ++e) out[e] = -S.lam[e];
@@ -1755,8 +1954,8 @@ struct Solver {
         double v[SD];
 #pragma unroll
         for (int e = 0; e < SD; ++e) v[e] = -S.ll[e] - (cp ? cp[e] : 0.0);
-        if (cp) v[0] += smu;
-        soc_iprod<SD>(S.lam, v, out);
+        if (cp && (!SPLIT || q == 0)) v[0] += smu;   // + smu e (the head coordinate)
+        ciprod(S.lam, v, out);
     }
     // SOC part of the step bound (soc_linesearch over the lane's blocks; ds/dz hold the
     // SOC rows only), as a running max of inverse bounds like the orthant's cmax
@@ -1766,7 +1965,7 @@ struct Solver {
     }
     DCOL_HD double soc_bound1(const SocNT& W, int b, const double* ds, const double* dz, double cmax) const {
         const int k0 = OR + SD * b;
-        const double ib = fmax(soc_ls_inv<SD>(s + k0, ds, W.lis[0], W.lrc[0]), soc_ls_inv<SD>(z + k0, dz, W.lis[1], W.lrc[1]));
+        const double ib = fmax(lsinv(s + k0, ds, W.lis[0], W.lrc[0]), lsinv(z + k0, dz, W.lis[1], W.lrc[1]));
         return vs[b] ? fmax(cmax, ib) : cmax;
     }
 
@@ -1880,6 +2079,14 @@ struct Solver {
             for (int c = 0; c < 3; ++c) g.u[c] = fma(zk, gr(k, c), g.u[c]);
         }
         }
+        if constexpr (SPLIT) {   // lane q holds coordinates 2q, 2q + 1 of the block
+            const bool own = vs[0] && soc_owner[0] == prim;
+            const double z0 = own ? (wt ? wt[OR] : z[OR]) : 0.0, z1 = own ? (wt ? wt[OR + 1] : z[OR + 1]) : 0.0;
+            g.zs[0] = q ? 0.0 : z0;
+            g.zs[1] = q ? 0.0 : z1;
+            g.zs[2] = q ? z0 : 0.0;
+            g.zs[3] = q ? z1 : 0.0;
+        } else
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
             const bool own = vs[b] && soc_owner[b] == prim;
@@ -2088,7 +2295,7 @@ struct Solver {
         SocNT W[SSA];
 #pragma unroll
         for (int b = 0; b < SS; ++b) {
-            soc_nt<SD>(s + OR + SD * b, z + OR + SD * b, W[b]);
+            nt(s + OR + SD * b, z + OR + SD * b, W[b]);
             soc_hadd(b, W[b], Hm);
         }
         allsum_sym(Hm);
@@ -2105,7 +2312,7 @@ struct Solver {
             double u[SD], t[SD];
 #pragma unroll
             for (int e = 0; e < SD; ++e) u[e] = rowdot(k0 + e, vimp);
-            soc_w2inv<SD>(W[b], u, t);
+            w2inv(W[b], u, t);
 #pragma unroll
             for (int e = 0; e < SD; ++e) wts[k0 + e] = vs[b] ? -t[e] : 0.0;
         }
@@ -2182,7 +2389,7 @@ DCOL_HD void launder(P& p) {
 // without DCOL_GRAD_ENVELOPE / DCOL_GRAD_IMPLICIT): the envelope and implicit code is not
 // compiled in, so its register pressure never shapes the FD path (variants.py BOX_FD)
 template <int N, int NSOC, int OMAX, int LPP, bool FULL = false, bool BALL = false, bool CONE = false, int OE = 0,
-          int MODE = 0, bool GLDS = false, bool BOX = false, bool FDONLY = false>
+          int MODE = 0, bool GLDS = false, bool BOX = false, bool FDONLY = false, bool SPLIT = false>
 DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1, int k1o = -1, int k2o = -1) {
     DCOL_STAMP(A, pi, q, 0);
     const int64_t B = A.B;
@@ -2205,7 +2412,7 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1, int k
     DCOL_STAMP(A, pi, q, 1);
 
     static_assert(!BOX || FULL, "BOX kernels are padding-free");
-    using Slv = Solver<N, NSOC, OMAX, LPP, BALL, CONE, OE, GLDS, BOX>;
+    using Slv = Solver<N, NSOC, OMAX, LPP, BALL, CONE, OE, GLDS, BOX, SPLIT>;
     Slv P;
     P.q = q;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -2366,7 +2573,8 @@ DCOL_HD void solve_one(const KArgs& A, int64_t pi, int q, int64_t ci = -1, int k
 constexpr int kSolveBlock = DCOL_BLOCK;
 static_assert(kSolveBlock % 64 == 0, "one or more whole waves per workgroup");
 
-// FL: variant flags, bit 0 FULL, bit 1 BALL, bit 2 CONE, bit 3 BOX, bit 6 FD-only gradient (variants.py)
+// FL: variant flags, bit 0 FULL, bit 1 BALL, bit 2 CONE, bit 3 BOX, bit 5 SPLIT ball block, bit 6 FD-only
+// gradient (variants.py)
 // OE > 0: the row-partitioned (PART) copy with OE extra-column row slots (Solver).
 // FL bit 4 (16): the main launch of a suspend / resume pair (solve_one MODE 1)
 // WPS >= 10: the LDS-rows copy (Solver GLDS) at WPS - 10 waves per SIMD (variants.py);
@@ -2384,7 +2592,7 @@ __global__ void __launch_bounds__(kSolveBlock, WPS % 10) prox_kernel(KArgs A) {
     if (slot >= A.n) return;
     const int64_t pi = A.perm ? (int64_t)A.perm[A.slot0 + slot] : (A.slot0 + slot);
     solve_one<N, NSOC, OMAX, LPP, (FL & 1) != 0, (FL & 2) != 0, (FL & 4) != 0, OE, (FL & 16) ? 1 : 0,
-              kGlds && WPS >= 10, (FL & 8) != 0, (FL & 64) != 0>(A, pi, q);
+              kGlds && WPS >= 10, (FL & 8) != 0, (FL & 64) != 0, (FL & 32) != 0>(A, pi, q);
 }
 
 // The resume launch of a suspend / resume pair: one lane group per continuation entry;

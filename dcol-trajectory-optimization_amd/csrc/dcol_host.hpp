@@ -183,6 +183,24 @@ inline bool part_disabled() {
     return off;
 }
 
+// DCOL_SPLIT=1: {capsule, cylinder} x polytope PART buckets with a split-SOC copy
+// (variants.py SPLIT) run it, at two lanes per pair (opt-in A/B; off by default)
+inline bool split_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("DCOL_SPLIT");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
+}
+inline bool split_built(int N, int nsoc, int omax, int oe) {
+    bool built = false;
+#define DCOL_SPB(NN, NS, OM, LP, WP, FL, OEE) \
+    if (NN == N && NS == nsoc && OM == omax && OEE == oe) built = true;
+    DCOL_SPLIT_VARIANTS(DCOL_SPB)
+#undef DCOL_SPB
+    return built;
+}
+
 // Compiled LPP of a PART bucket: the first listed (throughput choice), DCOL_LPP=<n> if that
 // one is compiled, or with latency = true the largest; 0 if the bucket has none (or not the
 // forced one)
@@ -202,6 +220,7 @@ inline int part_lpp(int N, int nsoc, int omax, int oe, bool latency = false) {
 #undef DCOL_PL
     if (latency) return best;
     if (forced) return hit;
+    if (split_enabled() && split_built(N, nsoc, omax, oe)) return 2;
     return first;
 }
 

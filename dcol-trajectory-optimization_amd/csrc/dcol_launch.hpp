@@ -5,7 +5,8 @@
 
 namespace dcol {
 // launch flags of a bucket (the variant flags FL of variants.py a launch may use)
-enum : int { LF_FULL = 1, LF_BALL = 2, LF_CONE = 4, LF_BOX = 8, LF_FDONLY = 64 };   // (LF_FDONLY: a run without envelope / implicit gradients)
+enum : int { LF_FULL = 1, LF_BALL = 2, LF_CONE = 4, LF_BOX = 8, LF_SPLIT = 32, LF_FDONLY = 64 };
+// (LF_FDONLY: a run without envelope / implicit gradients; LF_SPLIT: DCOL_SPLIT=1 opt-in)
 constexpr int kBlock = kSolveBlock;   // threads per workgroup of the solve kernel
 constexpr int kSideStreams = 7;   // capacity of the extra streams for concurrent variant launches
                                   // (dcol_capi.cpp side_streams(): 3 by default, DCOL_SIDE_STREAMS)

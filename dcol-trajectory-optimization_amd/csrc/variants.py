@@ -49,6 +49,7 @@ Generates dcol_variants.inc (FL = variant flags: bit 0 FULL, bit 1 BALL, bit 2 C
   DCOL_PART_SHAPES(X)    X(N, NSOC, OMAX, OE) once per PART bucket (host bucketing, emulator)
   DCOL_FUSED_PART_VARIANTS(X)  X(ID, N, NSOC, OMAX, LPP, FL, OE) the PART cases of the fused kernel
   DCOL_SUSP_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, FL, OE) suspend / resume copies (FL bit 4 = 16)
+  DCOL_SPLIT_VARIANTS(X)  X(N, NSOC, OMAX, LPP, WPS, FL, OE) split-SOC PART copies (FL bit 5 = 32)
   DCOL_PACKED_VARIANTS(X)  X(ID, N, NSOC, OMAX, LPP, FL, OE) the cases of the packed kernel
 
 SUSP variants (dcol_device.hpp KArgs susp_*, dcol_kernels_susp.hip): a large launch runs as a
@@ -235,6 +236,13 @@ def part_variants():
             for fl in part_flavours(n, s) for l, w in part_configs(n, s, o, oe, fl)]
 
 
+# SPLIT copies (Solver SPLIT, FL bit 5 = 32): {capsule, cylinder} x polytope
+# at two lanes per pair with the one ball SOC block split over both lanes (lane q holds its
+# coordinates 2q, 2q + 1) instead of lane 1 idling through the SOC work.  Opt-in (DCOL_SPLIT=1,
+# A/B: tools/class_bench.py); the buckets' default stays LPP 1 (PART above).
+SPLIT = [(5, 1, 8, 2, 1, 35, 2), (5, 1, 8, 2, 1, 34, 2), (5, 1, 8, 2, 2, 35, 2), (5, 1, 8, 2, 2, 34, 2),
+         (5, 1, 10, 2, 1, 35, 2), (5, 1, 10, 2, 1, 34, 2)]
+
 # (N, NSOC, OMAX, LPP, WPS, FL without the SUSP bit, OE): the benchmark's poly x poly kernel
 SUSP = [(4, 0, 12, 2, 2, 9, 0), (4, 0, 12, 2, 2, 1, 0)]   # the BOX copy first (box x box launches)
 
@@ -366,6 +374,8 @@ def main():
     lines += [f"    X({base + i}, {n}, {s}, {o}, {l}, {f}, {oe}) \\" for i, (n, s, o, l, f, oe) in enumerate(fused_part())]
     lines += ["", "#define DCOL_PACKED_VARIANTS(X) \\"]
     lines += [f"    X({i}, {n}, {s}, {o}, {l}, {fl}, {oe}) \\" for i, (n, s, o, l, fl, oe, _) in enumerate(packed())]
+    lines += ["", "#define DCOL_SPLIT_VARIANTS(X) \\"]
+    lines += [f"    X({n}, {s}, {o}, {l}, {w}, {fl}, {oe}) \\" for n, s, o, l, w, fl, oe in SPLIT]
     lines += ["", "#define DCOL_SUSP_VARIANTS(X) \\"]
     lines += [f"    X({n}, {s}, {o}, {l}, {w}, {fl | 16}, {oe}) \\" for n, s, o, l, w, fl, oe in SUSP]
     lines.append("")

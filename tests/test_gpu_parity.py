@@ -329,16 +329,19 @@ s1, s2 = np.tile(ids[d["s1"]], K), np.tile(ids[d["s2"]], K)
 r = eng.solve_host(s1, s2, np.tile(d["pose1"], (K, 1)), np.tile(d["pose2"], (K, 1)), grad="fd", contact=False)
 b = eng.plan(s1, s2).buckets()
 np.savez(sys.argv[1], alpha=r.alpha, grad=r.grad, iters=r.iters, status=r.status,
-         part=np.array([x["oe"] for x in b]), flags=np.array([x["flags"] for x in b]))
+         part=np.array([x["oe"] for x in b]), flags=np.array([x["flags"] for x in b]),
+         shape=np.array([(x["N"], x["nsoc"], x["lpp"]) for x in b]))
 """
 
 
-@pytest.mark.parametrize("var", ["DCOL_NO_BALL", "DCOL_NO_CONE", "DCOL_NO_PART"])
+@pytest.mark.parametrize("var", ["DCOL_NO_BALL", "DCOL_NO_CONE", "DCOL_NO_PART", "DCOL_SPLIT"])
 def test_mixed_golden_large_plan_env_variants(tmp_path, var):
     """The documented A/B switches on a plan large enough for the throughput buckets (the
     mixed golden set tiled to 150k pairs): DCOL_NO_BALL (no ball-row kernels: the x polytope
     row-partitioned buckets, compiled with ball rows only, must fall back to the dense rows
-    instead of failing the launch), DCOL_NO_CONE, DCOL_NO_PART -- status and iteration counts
+    instead of failing the launch), DCOL_NO_CONE, DCOL_NO_PART, DCOL_SPLIT (the {capsule,
+    cylinder} x polytope buckets at two lanes per pair with the ball SOC block split over
+    both, Solver SPLIT; rounding-level reordered sums) -- status and iteration counts
     equal to the reference's on every pair, alpha and gradient at the parity tolerances."""
     import os
     import subprocess
@@ -346,7 +349,8 @@ def test_mixed_golden_large_plan_env_variants(tmp_path, var):
 
     from conftest import PKG, REPO
     path = [p for p in golden_files() if p.endswith("synthetic_mixed.npz")][0]
-    env = {k: v for k, v in os.environ.items() if k not in ("DCOL_NO_BALL", "DCOL_NO_CONE", "DCOL_NO_PART", "DCOL_LPP")}
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("DCOL_NO_BALL", "DCOL_NO_CONE", "DCOL_NO_PART", "DCOL_LPP", "DCOL_SPLIT")}
     env[var] = "1"
     f = str(tmp_path / "out.npz")
     subprocess.run([sys.executable, "-c", _NO_BALL_SCRIPT, f, PKG, REPO, path], check=True, env=env, timeout=240)
@@ -363,3 +367,6 @@ def test_mixed_golden_large_plan_env_variants(tmp_path, var):
         assert not np.any((r["flags"] & 2) != 0)
     if var == "DCOL_NO_PART":
         assert not np.any(r["part"] > 0)
+    if var == "DCOL_SPLIT":   # the split copies ran: N = 5, one SOC block, PART, two lanes
+        sh = r["shape"]
+        assert np.any((sh[:, 0] == 5) & (sh[:, 1] == 1) & (r["part"] > 0) & (sh[:, 2] == 2))

@@ -8,7 +8,8 @@ count and its mix -- FP64 VALU, AGPR moves (v_accvgpr_read/write: values the reg
 allocator parked in AGPRs), DPP lane moves, selects, scratch traffic -- plus the kernel's
 register / scratch totals.  Used for the row-partition work.
 Usage: python3 tools/isa_stats.py N:NSOC:OMAX:LPP[:OE[:FL]] [--waves 1] ...
-  FL bits: 1 FULL, 2 BALL, 4 CONE, 8 BOX (as variants.py), 32 LDS rows (Solver GLDS; WPS >= 10 in variants.py)
+  FL bits: 1 FULL, 2 BALL, 4 CONE, 8 BOX, 64 FD-only (as variants.py), 32 LDS rows (Solver GLDS; WPS >= 10
+  in variants.py), 256 split ball SOC block (Solver SPLIT; variants.py FL bit 32)
 """
 import argparse
 import os
@@ -26,7 +27,7 @@ __global__ void __launch_bounds__(64, {w}) kb(KArgs A) {{
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t slot = t / {l}; const int q = (int)(t % {l});
     if (slot >= A.n) return;
-    solve_one<{n}, {s}, {o}, {l}, {full}, {ball}, {cone}, {oe}, 0, {glds}, {box}>(A, slot, q);
+    solve_one<{n}, {s}, {o}, {l}, {full}, {ball}, {cone}, {oe}, 0, {glds}, {box}, {fdonly}, {split}>(A, slot, q);
 }}
 }}
 """
@@ -49,7 +50,8 @@ def stats(spec, waves, extra=()):
         asm = os.path.join(tmp, "k.s")
         open(src, "w").write(SRC.format(n=n, s=s, o=o, l=l, oe=oe, w=waves, full="true" if fl & 1 else "false",
                                         ball="true" if fl & 2 else "false", cone="true" if fl & 4 else "false",
-                                        glds="true" if fl & 32 else "false", box="true" if fl & 8 else "false"))
+                                        glds="true" if fl & 32 else "false", box="true" if fl & 8 else "false",
+                                        fdonly="true" if fl & 64 else "false", split="true" if fl & 256 else "false"))
         r = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=on", f"-I{CSRC}",
                             *extra, "-S", "--offload-device-only", src, "-o", asm], capture_output=True, text=True)
         if r.returncode:

@@ -81,5 +81,17 @@ case $P in
       "sweep|700|python3 tools/shard_bench.py --sweep --worlds $W --only=default,pack_all,pack_off" \
       "trace125k|200|rocprofv3 --kernel-trace -f csv -d $O/trace125k -o run -- python3 tools/shard_bench.py --worlds 8 --steps 20" \
       "tests|900|python3 -u -m pytest tests -m gpu -q -s --timeout 300 --timeout-method thread -k \"$K\"" ;;
+  split)      # the split-SOC copies (DCOL_SPLIT=1, Solver SPLIT) of {capsule, cylinder} x polytope:
+              # parity (env-variant test) and per-class time against the default (LPP 1) and the
+              # two-lane copies without the split (DCOL_LPP=2)
+    C=capsule-polytope,polytope-capsule,cylinder-polytope,polytope-cylinder
+    CB="python3 tools/class_bench.py --small 0 --reps 20 --classes $C"
+    OUT=$O $S \
+      "tests|600|python3 -u -m pytest tests -m gpu -q -s --timeout 300 --timeout-method thread -k env_variants" \
+      "cls_default|300|$CB" \
+      "cls_split|300|DCOL_SPLIT=1 $CB" \
+      "cls_split_w2|300|DCOL_SPLIT=1 DCOL_WPS=2 $CB" \
+      "cls_lpp2|300|DCOL_LPP=2 $CB" \
+      "cls_default2|300|$CB" ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
