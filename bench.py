@@ -323,8 +323,15 @@ def main():
                       for st in lane_streams[1:]]
 
     settle = clock_settle(step, stream, dev, wd, args.settle_ms)
+    # the W warm-up steps in the same bracket as the timed steps (timing events, polled end,
+    # synchronize): the first such region of a process paid ~40 us more at its end than later
+    # ones (tools/region_probe.py), which K = 20 timed steps would otherwise carry
+    w_start, w_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    w_start.record(stream)
     for k in range(args.warmup):
         step()
+    w_end.record(stream)
+    wait_event(w_end, wd, "warmup", args.warmup - 1)
     sync(dev, wd, "warmup")
 
     # value: exactly K steps on ONE stream, barrier + synchronize on both sides.  kernel_ms =
@@ -569,8 +576,9 @@ def barrier(dist, wd, phase):
 
 
 def wait_event(e, wd, phase, step):
-    if wd is None:
-        e.synchronize()
+    if wd is None:   # polling, as the deadline's wait does (a blocking wait's wake-up adds
+        while not e.query():   # 10-15 us to the timed region, tools/step_latency.py)
+            pass
     else:
         wd.wait_event(e, phase, step)
 
