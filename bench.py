@@ -238,6 +238,8 @@ def main():
                     help="mixed1m: all-gather through torch.distributed instead of the C-ABI RCCL path")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process (HIP hardware queues; 0 = leave the environment's)")
+    ap.add_argument("--no-cost-order", dest="cost_order", action="store_false",
+                    help="skip the `cost_order` section (the pairing re-listed by iteration count, drifting poses)")
     ap.add_argument("--no-kernel-1m", dest="kernel_1m", action="store_false",
                     help="skip the 1M-pair kernel-only steady-state section (kernel_1m)")
     ap.add_argument("--deadline-s", type=float, default=float(os.environ.get("DCOL_BENCH_DEADLINE_S", "180")),
@@ -384,6 +386,8 @@ def main():
     # after end_to_end's host-side staging the GPU has idled and re-ramps through the first
     # ~10 ms of launches -- measured 0.44 ms per 1M launch there against 0.36 ms)
     k1m = kernel_1m(args, eng, ids, tab, dev) if world == 1 and args.kernel_1m else None
+    cord = (cost_order_section(args, eng, ids, s1, s2, p1, p2, dev)
+            if world == 1 and args.cost_order and args.max_iter == 50 else None)
     e2e = end_to_end(args, eng, ids, s1, s2, p1, p2, pose1, pose2, out, step, dev) if world == 1 else None
     if dist is not None:
         t = torch.tensor([elapsed, kern_ms, elapsed_pipe or 0.0], device=coll_dev, dtype=torch.float64)
@@ -461,6 +465,8 @@ def main():
         line["end_to_end"] = e2e
     if k1m is not None:
         line["kernel_1m"] = k1m
+    if cord is not None:
+        line["cost_order"] = cord
     # spot parity check against the oracle on the first and the last pairs of the timed batch
     # (a graded launch solves its last pairs with the wider lane groups)
     if args.check and args.max_iter == 50:
@@ -518,6 +524,10 @@ def summary(line):
     if "kernel_1m" in line:
         out["kernel_1m"] = {"pair_solves_per_s": line["kernel_1m"]["pair_solves_per_s"],
                             "fp64_frac": line["kernel_1m"]["roofline_fp64"]["frac"]}
+    if "cost_order" in line:
+        c = line["cost_order"]
+        out["cost_order"] = {"given_ms": c["given_order"]["kernel_ms"], "cost_ms": c["cost_order"]["kernel_ms"],
+                             "speedup": c["speedup"], "bitwise_equal": c["bitwise_equal"]}
     if d:
         out["dropin_us_per_call"] = {k: d[k]["us_per_call"] for k in ("proximity_mrp", "proximity_gradient") if k in d}
     if "altro" in line:
@@ -581,6 +591,67 @@ def wait_event(e, wd, phase, step):
             pass
     else:
         wd.wait_event(e, phase, step)
+
+
+def cost_order_section(args, eng, ids, s1, s2, p1, p2, dev, steps=100, ring=16, sr=0.02, sp=0.01):
+    """The listing order of the pairing (dcol_amd.cost_order; not `value`): a wave runs until
+    its slowest pair has converged, so pairs listed in descending order of their last
+    iteration counts fill waves with pairs of similar cost.  A trajectory optimiser's view:
+    the same pairs at poses that drift from step to step -- a random walk from the configs[3]
+    poses (r + N(0, sr), p + N(0, sp) per step; a ring of `ring` pose sets walked forth and
+    back, so consecutive steps differ by one step) -- solved K steps back to back (HIP events)
+    in the given order and in the order of the iteration counts of ONE solve at the first
+    poses (re-listed once: pairs, poses and outputs in the new order), with the outputs of
+    the last step compared bitwise."""
+    import torch
+    from dcol_amd import alloc_outputs, cost_order
+    rng = np.random.default_rng(17)
+    B = len(s1)
+    walk = [(p1, p2)]
+    for _ in range(ring - 1):
+        q1, q2 = walk[-1][0].copy(), walk[-1][1].copy()
+        for q in (q1, q2):
+            q[:, :3] += rng.normal(0, sr, (B, 3))
+            q[:, 3:] += rng.normal(0, sp, (B, 3))
+        walk.append((q1, q2))
+    seq = list(range(ring)) + list(range(ring - 2, 0, -1))
+    stream = torch.cuda.current_stream(dev)
+    res = {"poses": f"random walk from the configs[3] poses: r + N(0, {sr}), p + N(0, {sp}) per step, "
+                    f"{ring} pose sets forth and back", "steps": steps}
+    outs = {}
+    first = None
+    for name in ("given", "cost"):
+        order = np.arange(B) if name == "given" else cost_order(first)
+        plan = eng.plan(ids[s1[order]], ids[s2[order]], cache=False)
+        dp = [(torch.from_numpy(np.ascontiguousarray(x[order].T)).to(dev),
+               torch.from_numpy(np.ascontiguousarray(y[order].T)).to(dev)) for x, y in walk]
+        out = alloc_outputs(B, dev, want_grad=True, want_contact=False)
+        runs = [plan.bind(d1, d2, out, grad=args.grad, contact=False, stream=stream) for d1, d2 in dp]
+        runs[0]()
+        torch.cuda.synchronize(dev)
+        if first is None:
+            first = out["iters"].cpu().numpy()   # the one solve the cost order is taken from
+        for k in range(20):
+            runs[seq[k % len(seq)]]()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for k in range(steps):
+            runs[seq[k % len(seq)]]()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / steps
+        inv = np.empty(B, np.int64)
+        inv[order] = np.arange(B)
+        outs[name] = {k: (v.cpu().numpy()[..., inv]) for k, v in out.items()}
+        res[name + "_order"] = {"kernel_ms": ms, "pair_solves_per_s": B / (ms * 1e-3)}
+        del runs, dp, out, plan
+    res["bitwise_equal"] = all(np.array_equal(outs["given"][k].view(np.int64) if outs["given"][k].dtype == np.float64
+                                              else outs["given"][k],
+                                              outs["cost"][k].view(np.int64) if outs["cost"][k].dtype == np.float64
+                                              else outs["cost"][k]) for k in outs["given"])
+    res["speedup"] = res["given_order"]["kernel_ms"] / res["cost_order"]["kernel_ms"]
+    return res
 
 
 def kernel_1m(args, eng, ids, tab, dev, reps=20):

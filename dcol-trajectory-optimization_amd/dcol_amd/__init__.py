@@ -7,10 +7,10 @@ Host-side mirror of the reference's proximity API over the C-ABI of lib/libdcol.
 from . import _lib
 from ._lib import DcolLibraryError, device_count, load, status_string
 from .engine import (DEFAULT_MAX_ITER, DEFAULT_TOL, Engine, PDIPFailure, Plan, Result, Table,
-                     alloc_outputs, default_engine, raise_for_status)
+                     alloc_outputs, cost_order, default_engine, raise_for_status)
 from .shapes import ShapeSpec, make_descs, pose_of, shape_type, spec_from_arrays, spec_from_object
 
 __all__ = ["_lib", "DcolLibraryError", "device_count", "load", "status_string", "DEFAULT_MAX_ITER",
-           "DEFAULT_TOL", "Engine", "PDIPFailure", "Plan", "Result", "Table", "alloc_outputs",
+           "DEFAULT_TOL", "Engine", "PDIPFailure", "Plan", "Result", "Table", "alloc_outputs", "cost_order",
            "default_engine", "raise_for_status", "ShapeSpec", "make_descs", "pose_of", "shape_type",
            "spec_from_arrays", "spec_from_object"]

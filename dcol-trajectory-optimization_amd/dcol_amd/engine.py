@@ -237,6 +237,21 @@ def alloc_outputs(B: int, device, want_grad=True, want_contact=True):
     return out
 
 
+def cost_order(iters) -> np.ndarray:
+    """A listing order for a fixed pairing: pair indices in descending order of their last
+    Newton iteration counts (stable).  A wave of a solve launch runs until its slowest pair
+    has converged, so pairs listed (and their poses and outputs laid out) in this order fill
+    each wave with pairs of similar cost, the slowest first; a plan built on the re-listed
+    pairing solves the same pairs with bitwise the same results.  For a trajectory optimiser
+    (the same pairs at slowly changing poses) re-list once from a solve's `iters` and keep
+    the order -- measured on configs[3] at drifting poses: bench.py `cost_order`,
+    tools/order_probe.py.  The plan itself cannot reorder slots for free: a permutation read
+    through an index array turns the coalesced pose / output accesses into gathers and
+    scatters, which cost more than the order saves."""
+    it = np.asarray(iters).reshape(-1)
+    return np.argsort(-it.astype(np.int64), kind="stable")
+
+
 class Engine:
     """Shape registry + lazily (re)built device table.
 
