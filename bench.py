@@ -1144,7 +1144,8 @@ def shards_section(args, eng, ids, tab, s1, s2, p1, p2, cost, dev):
         d2 = torch.from_numpy(np.ascontiguousarray(p2[mine].T)).to(dev)
         out = alloc_outputs(len(mine), dev, want_grad=True, want_contact=False)
         run = plan.bind(d1, d2, out, grad=args.grad, contact=False, stream=stream)
-        for _ in range(5):
+        clock_settle(run, stream, dev, None, 10.0)   # (as tools/shard_bench.py: each plan from settled clocks)
+        for _ in range(10):
             run()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
