@@ -238,6 +238,9 @@ def main():
                     help="mixed1m: all-gather through torch.distributed instead of the C-ABI RCCL path")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process (HIP hardware queues; 0 = leave the environment's)")
+    ap.add_argument("--timed-outputs", choices=("reference", "all"), default="reference",
+                    help="configs[3]: the outputs the timed steps write -- alpha + gradient, what the reference's "
+                         "proximity_gradient returns (default), or also the per-pair status / iteration counts")
     ap.add_argument("--no-cost-order", dest="cost_order", action="store_false",
                     help="skip the `cost_order` section (the pairing re-listed by iteration count, drifting poses)")
     ap.add_argument("--no-kernel-1m", dest="kernel_1m", action="store_false",
@@ -316,11 +319,18 @@ def main():
     out = alloc_outputs(B, dev, want_grad=True, want_contact=False)
     stream = torch.cuda.current_stream(dev)
 
-    step = plan.bind(pose1, pose2, out, grad=args.grad, contact=False, stream=stream, max_iter=args.max_iter)
+    # the timed steps write what the reference's proximity_gradient returns -- alpha and the
+    # gradient (--timed-outputs reference, the default); the per-pair status and Newton
+    # iteration counts (optional outputs, 8 B per pair) come from one untimed step after them
+    stats_out = ("iters", "status") if args.timed_outputs == "reference" else ()
+    out_t = {k: v for k, v in out.items() if k not in stats_out}
+    step = plan.bind(pose1, pose2, out_t, grad=args.grad, contact=False, stream=stream, max_iter=args.max_iter)
     # pipelined issue: S streams, each with its own outputs (poses are read-only, shared)
     S = max(1, args.streams)
     lane_streams = [stream] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
-    lanes = [step] + [plan.bind(pose1, pose2, alloc_outputs(B, dev, want_grad=True, want_contact=False),
+    lanes = [step] + [plan.bind(pose1, pose2, {k: v for k, v in alloc_outputs(B, dev, want_grad=True,
+                                                                            want_contact=False).items()
+                                              if k not in stats_out},
                                 grad=args.grad, contact=False, stream=st, max_iter=args.max_iter)
                       for st in lane_streams[1:]]
 
@@ -388,7 +398,7 @@ def main():
     k1m = kernel_1m(args, eng, ids, tab, dev) if world == 1 and args.kernel_1m else None
     cord = (cost_order_section(args, eng, ids, s1, s2, p1, p2, dev)
             if world == 1 and args.cost_order and args.max_iter == 50 else None)
-    e2e = end_to_end(args, eng, ids, s1, s2, p1, p2, pose1, pose2, out, step, dev) if world == 1 else None
+    e2e = end_to_end(args, eng, ids, s1, s2, p1, p2, pose1, pose2, out_t, step, dev) if world == 1 else None
     if dist is not None:
         t = torch.tensor([elapsed, kern_ms, elapsed_pipe or 0.0], device=coll_dev, dtype=torch.float64)
         with guard(wd, "all_reduce of the timings"):
@@ -398,6 +408,9 @@ def main():
     else:
         kern_ms_max = kern_ms
 
+    # one untimed step with every output (the timed ones left status / iters unwritten)
+    plan.bind(pose1, pose2, out, grad=args.grad, contact=False, stream=stream, max_iter=args.max_iter)()
+    sync(dev, wd, "the statistics step")
     status = out["status"].cpu().numpy()
     iters = out["iters"].cpu().numpy()
     alpha = out["alpha"].cpu().numpy()
@@ -448,6 +461,8 @@ def main():
         "timing": "value = pairs / ms_per_step of K steps on one stream; kernel_ms = the HIP-event time of that same "
                   "timed region on the launch stream / K (the per-launch duration of the back-to-back launches), the "
                   "rooflines' time base",
+        "timed_outputs": ("alpha + gradient (the reference's outputs); status / iters from one untimed step after the "
+                          "timed ones" if stats_out else "alpha, gradient, status, iters"),
         "pipeline": {"streams": S, "note": "the same K steps issued round-robin on S streams with separate outputs "
                      "(an overlap rate: one step's last round of waves overlaps the next step's first; not value)",
                      "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),

@@ -187,7 +187,8 @@ class Plan:
              stream=None):
         """Pre-convert every argument of dcol_plan_run once; returns a zero-argument callable
         that re-launches the solve on the same device buffers (hot loops: ALTRO phases,
-        bench.py).  Validates like run()."""
+        bench.py).  Validates like run().  `out` without "iters" / "status": those per-pair
+        outputs are not written (dcol_plan_run takes NULL for them)."""
         import torch
         B = self.B
         dev = torch.device("cuda", self.table.device)
@@ -204,7 +205,7 @@ class Plan:
         ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
         args = (self.handle, ptr(pose1), ptr(pose2), ctypes.c_double(tol), ctypes.c_int32(max_iter),
                 ctypes.c_int32(flags), ptr(out["alpha"]), ptr(out.get("contact")), ptr(out.get("grad")),
-                ptr(out["iters"]), ptr(out["status"]), ctypes.c_void_p(stream.cuda_stream))
+                ptr(out.get("iters")), ptr(out.get("status")), ctypes.c_void_p(stream.cuda_stream))
         fn = _lib.load().dcol_plan_run
         keep = (self, pose1, pose2, out)
 
